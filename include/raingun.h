@@ -1,0 +1,212 @@
+/*
+ * raingun.h — C ABI of the MI355X-native renderer for raingun's per-pixel
+ * ray-trace path (libraingun_hip.so).
+ *
+ * The reference has no FFI layer: the seam this ABI replaces is the Rust
+ * function
+ *     rendering::render_image(scene: &Scene, width: u32, height: u32)
+ *         -> ImageBuffer<Rgba<u8>, Vec<u8>>          raingun-lib/src/rendering.rs:24-38
+ * reached through Scene::render_image (raingun-lib/src/scene.rs:41-43) from
+ * the batch driver (src/render.rs:55).  Everything below that call
+ * (render_pixel / get_color / cast_ray / shade_diffuse / fresnel and the body,
+ * ray, light, material and colour primitives) runs inside one HIP megakernel
+ * for gfx950.
+ *
+ * All plain C: pointers, sizes, POD structs.  No torch types, no C++.
+ * Paths are relative to /root/reference.
+ */
+#ifndef RAINGUN_H
+#define RAINGUN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RG_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------
+ * Status codes.  The reference panics; the ABI returns one negative code per
+ * panic site instead (no exception or abort ever crosses the boundary).
+ * ---------------------------------------------------------------------- */
+typedef enum rg_status {
+    RG_OK = 0,
+    RG_ERR_INVALID_ARGUMENT = -1,   /* null pointers, zero sizes, bad enum values */
+    RG_ERR_PORTRAIT = -2,           /* assert!(width >= height)          ray.rs:42 */
+    RG_ERR_AABB_NORMAL = -3,        /* "Could not determine normal"       bodies.rs:324 */
+    RG_ERR_NAN_DISTANCE = -4,       /* partial_cmp(..).unwrap() on NaN    scene.rs:38 */
+    RG_ERR_TRANSMISSION = -5,       /* create_transmission(..).unwrap()   rendering.rs:106 */
+    RG_ERR_TEXTURE = -6,            /* texture index out of range / empty image (material.rs:34-47) */
+    RG_ERR_DEVICE = -10,            /* HIP runtime error */
+    RG_ERR_OUT_OF_MEMORY = -11,
+    RG_ERR_CANCELLED = -12          /* streaming receiver dropped         rendering.rs:53-54 */
+} rg_status;
+
+/* ------------------------------------------------------------------------
+ * Flat POD scene description — mirrors `Scene` (scene.rs:11-19) after serde
+ * has run: bodies and lights in YAML order, textures already decoded to RGBA8
+ * (material.rs:34-47 decodes eagerly at load time).
+ * ---------------------------------------------------------------------- */
+enum rg_body_kind {            /* bodies.rs:41-47 */
+    RG_BODY_SPHERE = 0,        /* p = {center.x, center.y, center.z, radius}                 */
+    RG_BODY_PLANE = 1,         /* p = {origin.x, origin.y, origin.z, normal.x, normal.y, normal.z} */
+    RG_BODY_DISK = 2,          /* p = {origin.xyz, normal.xyz, radius}                        */
+    RG_BODY_AABB = 3           /* p = {bounds[0].xyz, bounds[1].xyz}                          */
+};
+
+enum rg_coloration_kind {      /* material.rs:79-83 */
+    RG_COLORATION_COLOR = 0,
+    RG_COLORATION_TEXTURE = 1
+};
+
+enum rg_surface_kind {         /* material.rs:108-113 */
+    RG_SURFACE_DIFFUSE = 0,
+    RG_SURFACE_REFLECTING = 1,
+    RG_SURFACE_REFRACTIVE = 2
+};
+
+enum rg_light_kind {           /* lights.rs:22-26 */
+    RG_LIGHT_DIRECTIONAL = 0,  /* v = direction */
+    RG_LIGHT_SPHERICAL = 1     /* v = position  */
+};
+
+typedef struct rg_material {   /* material.rs:66-71 */
+    uint32_t coloration;       /* rg_coloration_kind */
+    float color[3];            /* Coloration::Color, f32 RGB in [0,1] (color.rs:7-11) */
+    int32_t texture;           /* Coloration::Texture: index into rg_scene_desc.textures */
+    float x_offset, y_offset;  /* Texture::{x_offset,y_offset} (material.rs:89-90) */
+    float albedo;
+    uint32_t surface;          /* rg_surface_kind */
+    float reflectivity;        /* Surface::Reflecting */
+    float index;               /* Surface::Refractive */
+    float transparency;        /* Surface::Refractive */
+} rg_material;
+
+typedef struct rg_body {
+    uint32_t kind;             /* rg_body_kind */
+    uint32_t _pad;
+    double p[7];
+    rg_material material;
+} rg_body;
+
+typedef struct rg_light {      /* lights.rs:8-20 */
+    uint32_t kind;             /* rg_light_kind */
+    float color[3];
+    float intensity;
+    uint32_t _pad;
+    double v[3];
+} rg_light;
+
+typedef struct rg_texture {    /* decoded DynamicImage, RGBA8 row-major, width*height*4 bytes */
+    uint32_t width, height;
+    const uint8_t *rgba;
+} rg_texture;
+
+typedef struct rg_scene_desc { /* scene.rs:11-19; defaults scene.rs:21-31 */
+    double fov;                /* degrees, default 90 */
+    float default_color[3];    /* default black */
+    uint32_t max_recursion_depth; /* default 10 */
+    uint32_t n_bodies;
+    const rg_body *bodies;
+    uint32_t n_lights;
+    const rg_light *lights;
+    uint32_t n_textures;
+    const rg_texture *textures;
+} rg_scene_desc;
+
+/* Ray counts by class.  A ray is one Scene::trace call (scene.rs:34-39):
+ * primary rendering.rs:73, shadow rendering.rs:150, secondary rendering.rs:126. */
+typedef struct rg_ray_counts {
+    uint64_t primary;
+    uint64_t shadow;
+    uint64_t secondary;
+} rg_ray_counts;
+
+typedef struct rg_stats {
+    rg_ray_counts rays;
+    float kernel_ms;           /* HIP-event time of the render launch(es) on the render stream */
+    int32_t error_pixel;       /* first pixel (linear index) that raised a device error, or -1 */
+    uint32_t _pad;
+} rg_stats;
+
+/* Row selection for sharded renders: the frame is cut into tiles of
+ * `tile_rows` rows; this call renders tiles t with t % tile_stride == tile_offset,
+ * packed densely into the output in increasing t (the last tile may be partial
+ * and is zero-padded in the output to a full tile).  {tile_rows=height,
+ * tile_stride=1, tile_offset=0} is the whole frame.  */
+typedef struct rg_tiling {
+    uint32_t tile_rows;
+    uint32_t tile_stride;
+    uint32_t tile_offset;
+} rg_tiling;
+
+typedef struct rg_scene rg_scene;   /* opaque device-resident scene */
+
+/* ---------------------------------------------------------------- API */
+
+int32_t rg_abi_version(void);
+const char *rg_status_string(int32_t status);
+
+/* Number of HIP devices visible (0 if none / runtime missing). */
+int32_t rg_device_count(void);
+
+/* Copy the scene to `device` (SoA body tables, material/light tables, RGBA8
+ * textures).  The caller keeps ownership of `desc` and its arrays.
+ * Replaces Scene's deserialised in-memory form (scene.rs:11-19). */
+rg_status rg_scene_create(const rg_scene_desc *desc, int32_t device, rg_scene **out);
+void rg_scene_destroy(rg_scene *scene);
+
+/* Override the recursion cap of an uploaded scene (main.rs:119-123 clamps it;
+ * the depth-5 configs set it directly, scene.rs:16 is a pub field). */
+rg_status rg_scene_set_max_depth(rg_scene *scene, uint32_t max_recursion_depth);
+
+/* Blocking whole-frame render into a caller-owned host buffer of
+ * width*height*4 bytes (row-major RGBA8, alpha 255).
+ * Replaces rendering::render_image (rendering.rs:24-38). `stats` may be NULL. */
+rg_status rg_render_image(const rg_scene *scene, uint32_t width, uint32_t height,
+                          uint8_t *rgba_out, rg_stats *stats);
+
+/* Device-resident variant used by sharded / benchmark callers: renders the
+ * tiles selected by `tiling` into `rgba_dev` (device pointer on the scene's
+ * device, tiles_selected*tile_rows*width*4 bytes), on HIP stream `stream`
+ * (a hipStream_t; NULL = null stream).  `rgb_dev` (nullable, device) receives
+ * the pre-quantisation f32 RGB (3 floats per pixel, same packing) for float
+ * parity checks.  Asynchronous unless `stats` is non-NULL, in which case the
+ * call synchronises `stream` and fills ray counts, kernel time and errors. */
+rg_status rg_render_tiles_async(const rg_scene *scene, uint32_t width, uint32_t height,
+                                const rg_tiling *tiling, uint8_t *rgba_dev, float *rgb_dev,
+                                void *stream, rg_stats *stats);
+
+/* Host-buffer variant of rg_render_tiles_async (blocking).  rgb_out nullable. */
+rg_status rg_render_tiles(const rg_scene *scene, uint32_t width, uint32_t height,
+                          const rg_tiling *tiling, uint8_t *rgba_out, float *rgb_out,
+                          rg_stats *stats);
+
+/* Number of output rows a tiling produces for `height` (tiles selected * tile_rows). */
+uint32_t rg_tiling_rows(uint32_t height, const rg_tiling *tiling);
+
+/* Tile-completion streaming (replaces render_image_stream, rendering.rs:40-69,
+ * which sends one RenderedPixel per pixel over an mpsc channel): the frame is
+ * rendered in bands of `tile_rows` rows; after each band `on_tile` receives the
+ * band's RGBA8 rows on the host.  A non-zero return from `on_tile` cancels the
+ * remaining bands (the reference's `.all` stops when the channel closes) and
+ * the call returns RG_ERR_CANCELLED. */
+typedef int32_t (*rg_tile_callback)(uint32_t row_begin, uint32_t rows, uint32_t width,
+                                    const uint8_t *rgba, void *user);
+rg_status rg_render_stream(const rg_scene *scene, uint32_t width, uint32_t height,
+                           uint32_t tile_rows, rg_tile_callback on_tile, void *user,
+                           rg_stats *stats);
+
+/* Closest-hit query over all bodies (Scene::trace, scene.rs:34-39) for n rays
+ * given as {origin.xyz, direction.xyz} doubles (host buffers).  dist[i] is the
+ * hit distance and body[i] the body index, or body[i] = -1 on a miss. */
+rg_status rg_trace(const rg_scene *scene, const double *rays, uint32_t n,
+                   double *dist, int32_t *body);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RAINGUN_H */

@@ -1,0 +1,191 @@
+"""ctypes mirror of include/raingun.h and the loader for libraingun_hip.so.
+
+The product path is the HIP library.  There is no CPU fallback: if the
+shared object is missing or fails to load, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+LIB_PATH = PKG_DIR / "libraingun_hip.so"
+
+# ---------------------------------------------------------------- enums
+RG_OK = 0
+RG_ERR_INVALID_ARGUMENT = -1
+RG_ERR_PORTRAIT = -2
+RG_ERR_AABB_NORMAL = -3
+RG_ERR_NAN_DISTANCE = -4
+RG_ERR_TRANSMISSION = -5
+RG_ERR_TEXTURE = -6
+RG_ERR_DEVICE = -10
+RG_ERR_OUT_OF_MEMORY = -11
+RG_ERR_CANCELLED = -12
+
+BODY_SPHERE, BODY_PLANE, BODY_DISK, BODY_AABB = 0, 1, 2, 3
+COLORATION_COLOR, COLORATION_TEXTURE = 0, 1
+SURFACE_DIFFUSE, SURFACE_REFLECTING, SURFACE_REFRACTIVE = 0, 1, 2
+LIGHT_DIRECTIONAL, LIGHT_SPHERICAL = 0, 1
+
+
+# ---------------------------------------------------------------- structs
+class rg_material(C.Structure):
+    _fields_ = [
+        ("coloration", C.c_uint32),
+        ("color", C.c_float * 3),
+        ("texture", C.c_int32),
+        ("x_offset", C.c_float),
+        ("y_offset", C.c_float),
+        ("albedo", C.c_float),
+        ("surface", C.c_uint32),
+        ("reflectivity", C.c_float),
+        ("index", C.c_float),
+        ("transparency", C.c_float),
+    ]
+
+
+class rg_body(C.Structure):
+    _fields_ = [
+        ("kind", C.c_uint32),
+        ("_pad", C.c_uint32),
+        ("p", C.c_double * 7),
+        ("material", rg_material),
+    ]
+
+
+class rg_light(C.Structure):
+    _fields_ = [
+        ("kind", C.c_uint32),
+        ("color", C.c_float * 3),
+        ("intensity", C.c_float),
+        ("_pad", C.c_uint32),
+        ("v", C.c_double * 3),
+    ]
+
+
+class rg_texture(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("rgba", C.POINTER(C.c_uint8))]
+
+
+class rg_scene_desc(C.Structure):
+    _fields_ = [
+        ("fov", C.c_double),
+        ("default_color", C.c_float * 3),
+        ("max_recursion_depth", C.c_uint32),
+        ("n_bodies", C.c_uint32),
+        ("bodies", C.POINTER(rg_body)),
+        ("n_lights", C.c_uint32),
+        ("lights", C.POINTER(rg_light)),
+        ("n_textures", C.c_uint32),
+        ("textures", C.POINTER(rg_texture)),
+    ]
+
+
+class rg_ray_counts(C.Structure):
+    _fields_ = [("primary", C.c_uint64), ("shadow", C.c_uint64), ("secondary", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {"primary": int(self.primary), "shadow": int(self.shadow), "secondary": int(self.secondary)}
+
+    def total(self) -> int:
+        return int(self.primary) + int(self.shadow) + int(self.secondary)
+
+
+class rg_stats(C.Structure):
+    _fields_ = [
+        ("rays", rg_ray_counts),
+        ("kernel_ms", C.c_float),
+        ("error_pixel", C.c_int32),
+        ("_pad", C.c_uint32),
+    ]
+
+
+class rg_tiling(C.Structure):
+    _fields_ = [("tile_rows", C.c_uint32), ("tile_stride", C.c_uint32), ("tile_offset", C.c_uint32)]
+
+
+TILE_CALLBACK = C.CFUNCTYPE(C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8), C.c_void_p)
+
+# Every symbol include/raingun.h declares (tests/test_abi.py checks the export table).
+EXPORTED_SYMBOLS = (
+    "rg_abi_version",
+    "rg_status_string",
+    "rg_device_count",
+    "rg_scene_create",
+    "rg_scene_destroy",
+    "rg_scene_set_max_depth",
+    "rg_render_image",
+    "rg_render_tiles_async",
+    "rg_render_tiles",
+    "rg_tiling_rows",
+    "rg_render_stream",
+    "rg_trace",
+)
+
+
+class RaingunError(RuntimeError):
+    """A non-zero rg_status (the reference would have panicked)."""
+
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = status_string(status) if _LIB is not None else str(status)
+        super().__init__(f"{what}: {msg} (status {status})" if what else f"{msg} (status {status})")
+
+
+_LIB: C.CDLL | None = None
+
+
+def _declare(lib: C.CDLL) -> None:
+    P = C.POINTER
+    lib.rg_abi_version.restype = C.c_int32
+    lib.rg_status_string.restype = C.c_char_p
+    lib.rg_status_string.argtypes = [C.c_int32]
+    lib.rg_device_count.restype = C.c_int32
+    lib.rg_scene_create.restype = C.c_int32
+    lib.rg_scene_create.argtypes = [P(rg_scene_desc), C.c_int32, P(C.c_void_p)]
+    lib.rg_scene_destroy.restype = None
+    lib.rg_scene_destroy.argtypes = [C.c_void_p]
+    lib.rg_scene_set_max_depth.restype = C.c_int32
+    lib.rg_scene_set_max_depth.argtypes = [C.c_void_p, C.c_uint32]
+    lib.rg_render_image.restype = C.c_int32
+    lib.rg_render_image.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, P(rg_stats)]
+    lib.rg_render_tiles_async.restype = C.c_int32
+    lib.rg_render_tiles_async.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(rg_tiling), C.c_void_p,
+                                          C.c_void_p, C.c_void_p, P(rg_stats)]
+    lib.rg_render_tiles.restype = C.c_int32
+    lib.rg_render_tiles.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(rg_tiling), C.c_void_p, C.c_void_p,
+                                    P(rg_stats)]
+    lib.rg_tiling_rows.restype = C.c_uint32
+    lib.rg_tiling_rows.argtypes = [C.c_uint32, P(rg_tiling)]
+    lib.rg_render_stream.restype = C.c_int32
+    lib.rg_render_stream.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, TILE_CALLBACK, C.c_void_p,
+                                     P(rg_stats)]
+    lib.rg_trace.restype = C.c_int32
+    lib.rg_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+
+
+def lib() -> C.CDLL:
+    """Load libraingun_hip.so (built by ``make -C raingun_amd/csrc``).  Raises if absent."""
+    global _LIB
+    if _LIB is None:
+        path = os.environ.get("RAINGUN_HIP_LIB", str(LIB_PATH))
+        if not Path(path).exists():
+            raise RuntimeError(
+                f"{path} is missing: build it with `make -C raingun_amd/csrc` (or __graft_entry__.build()). "
+                "There is no CPU fallback for the render path.")
+        lib_ = C.CDLL(path)
+        _declare(lib_)
+        _LIB = lib_
+    return _LIB
+
+
+def status_string(status: int) -> str:
+    return lib().rg_status_string(int(status)).decode()
+
+
+def check(status: int, what: str = "") -> None:
+    if status != RG_OK:
+        raise RaingunError(status, what)

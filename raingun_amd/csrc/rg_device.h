@@ -1,0 +1,100 @@
+// rg_device.h — device-side scene layout shared by the render kernels and the
+// C-ABI host code in rg_capi.hip.  gfx950 only.
+//
+// HBM layout of an uploaded scene (one rg_scene per device):
+//   * hot tables (read by every ray, wave-uniform index -> scalar loads through
+//     the constant address space, SGPR operands straight into v_*_f64):
+//       sph[n_sph]   {cx, cy, cz, r*r}                 32 B  (bodies.rs:92-97)
+//       sph_cc[n_sph] (cx*cx + cy*cy) + cz*cz           8 B   primary-ray shortcut
+//       pln[n_pln]   {ox,oy,oz, nx,ny,nz, o.n, -}       64 B  (bodies.rs:136-149)
+//       dsk[n_dsk]   {ox,oy,oz, nx,ny,nz, r, o.n}       64 B  (bodies.rs:173-192)
+//       box[n_box]   {lo.xyz, hi.xyz}                   48 B  (bodies.rs:242-282)
+//     each with an int id table giving the body's index in YAML order (the
+//     closest-hit tie-break of scene.rs:34-39 is "first minimum in list order").
+//   * cold tables (per-lane gathers at shading time, L2 resident):
+//       bodies[n] {kind, params[7]}, mats[n] (one material per body),
+//       lights[n_lights], textures (RGBA8 texels, one u32 per texel).
+#pragma once
+#include <stdint.h>
+
+// Hot tables are read through the constant address space (addrspace 4) in
+// device code: with a wave-uniform index that always lowers to s_load_* (SGPR
+// operands, scalar cache), never to per-lane vector loads.
+#ifdef __HIP_DEVICE_COMPILE__
+#define RG_CONST __attribute__((address_space(4)))
+#else
+#define RG_CONST
+#endif
+template <class T>
+__device__ __forceinline__ const RG_CONST T *rg_cptr(const T *p) { return (const RG_CONST T *)p; }
+
+struct alignas(16) RgSph { double cx, cy, cz, r2; };
+struct alignas(16) RgPln { double ox, oy, oz, nx, ny, nz, on, pad; };
+struct alignas(16) RgDsk { double ox, oy, oz, nx, ny, nz, r, on; };
+struct alignas(16) RgBox { double lo[3], hi[3]; };
+
+struct RgBodyDev {         // per body, YAML order
+    int32_t kind;
+    int32_t pad;
+    double p[7];
+};
+
+struct RgMatDev {          // material.rs:66-71, flattened
+    int32_t coloration;
+    float color[3];
+    int32_t tex;
+    float xoff, yoff;
+    float albedo;
+    int32_t surface;
+    float reflectivity;
+    float index;
+    float transparency;
+};
+
+struct RgLightDev {        // lights.rs:8-26
+    int32_t kind;
+    float color[3];
+    float intensity;
+    int32_t pad;
+    double v[3];
+};
+
+struct RgTexDev {
+    const uint32_t *texels;  // RGBA8 packed little-endian: r | g<<8 | b<<16 | a<<24
+    int32_t w, h;
+};
+
+// Everything a render launch needs, passed by value as the kernel argument.
+struct RgKernelArgs {
+    // hot tables
+    const RgSph *sph;
+    const double *sph_cc;
+    const int32_t *sph_id;
+    const RgPln *pln;
+    const int32_t *pln_id;
+    const RgDsk *dsk;
+    const int32_t *dsk_id;
+    const RgBox *box;
+    const int32_t *box_id;
+    int32_t n_sph, n_pln, n_dsk, n_box;
+    // cold tables
+    const RgBodyDev *bodies;
+    const RgMatDev *mats;
+    const RgLightDev *lights;
+    const RgTexDev *texs;
+    int32_t n_bodies, n_lights;
+    // frame
+    uint32_t width, height;
+    uint32_t tile_rows, tile_stride, tile_offset, out_rows;
+    double fov_adjustment;   // tan(fov.to_radians() / 2), ray.rs:45 (host libm)
+    double aspect;           // width / height, ray.rs:43
+    float def[3];            // scene.default_color
+    uint32_t max_depth;      // scene.max_recursion_depth
+    // outputs
+    uint32_t *rgba;          // packed RGBA8, out_rows * width
+    float *rgb;              // nullable, out_rows * width * 3
+    unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=error key
+};
+
+// error key: (pixel << 8) | (-status); atomicMin keeps the lowest pixel.
+#define RG_ERRKEY_NONE 0xFFFFFFFFFFFFFFFFull

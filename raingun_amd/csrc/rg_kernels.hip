@@ -1,0 +1,624 @@
+// rg_kernels.hip — the render megakernel for gfx950 (MI355X).
+//
+// One lane = one pixel.  A wave covers an 8x8 pixel quad (ray coherence), a
+// 256-thread workgroup a 16x16 tile.  The reference's recursion
+//   render_pixel -> get_color -> {shade_diffuse | cast_ray -> get_color ...}
+// (raingun-lib/src/rendering.rs:71-172) becomes a per-lane state machine:
+// every loop iteration each live lane owns exactly ONE query ray (closest-hit
+// or shadow) and all lanes of the wave walk the body tables together, with a
+// wave-uniform body index, so body parameters come in through the scalar
+// cache as SGPR operands and the only divergence is in shading.
+//
+// Post-order evaluation with an explicit frame stack reproduces the
+// reference's f32 colour composition bit for bit (same operations, same
+// order), so the RGBA8 output is byte-identical to the CPU restatement.
+//
+// Numerics: -ffp-contract=off (and the pragma below): every f64/f32 multiply
+// and add is rounded separately, exactly as the reference's unfused Rust.
+// Division and sqrt are the correctly-rounded hipcc expansions.
+#include <hip/hip_runtime.h>
+
+#include "../../include/raingun.h"
+#include "rg_device.h"
+
+#pragma clang fp contract(off)
+
+namespace rgk {
+
+constexpr double SHADOW_BIAS = 1e-13;                 // lib.rs:11
+constexpr float PI_F = 3.14159265358979323846f;       // std::f32::consts::PI
+
+enum : int { MODE_CLOSEST = 0, MODE_SHADOW = 1, MODE_DONE = 2 };
+enum : int { FR_REFL = 0, FR_REFR_T = 1, FR_REFR_R = 2 };
+
+struct V3 { double x, y, z; };
+struct C3 { float r, g, b; };
+
+__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 scl(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ V3 normalize(V3 a) { return scl(a, 1.0 / sqrt(dot(a, a))); }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+
+__device__ __forceinline__ C3 c3(float r, float g, float b) { return C3{r, g, b}; }
+__device__ __forceinline__ C3 cadd(C3 a, C3 b) { return c3(a.r + b.r, a.g + b.g, a.b + b.b); }
+__device__ __forceinline__ C3 cmul(C3 a, C3 b) { return c3(a.r * b.r, a.g * b.g, a.b * b.b); }
+__device__ __forceinline__ C3 cscl(C3 a, float s) { return c3(a.r * s, a.g * s, a.b * s); }
+__device__ __forceinline__ C3 cclamp(C3 a) {  // color.rs:39-43 (f32::min/max ignore NaN)
+    return c3(fmaxf(fminf(a.r, 1.0f), 0.0f), fmaxf(fminf(a.g, 1.0f), 0.0f), fmaxf(fminf(a.b, 1.0f), 0.0f));
+}
+
+// Rust `f32 as u8` / `f32 as i32`: truncate, saturate, NaN -> 0.
+__device__ __forceinline__ uint32_t f32_to_u8(float v) {
+    if (!(v > 0.0f)) return 0u;
+    if (v >= 255.0f) return 255u;
+    return (uint32_t)v;
+}
+__device__ __forceinline__ int32_t f32_to_i32(float v) {
+    if (v != v) return 0;
+    if (v >= 2147483648.0f) return 2147483647;
+    if (v < -2147483648.0f) return (-2147483647 - 1);
+    return (int32_t)v;
+}
+
+__device__ __forceinline__ void raise_error(const RgKernelArgs &a, uint32_t pixel, int status) {
+    unsigned long long key = ((unsigned long long)pixel << 8) | (unsigned long long)(-status);
+    atomicMin(&a.counters[3], key);
+}
+
+// ---------------------------------------------------------------- closest hit
+// Scene::trace (scene.rs:34-39): first minimum in list order.  The body tables
+// are grouped by kind, so ties across groups are broken by the YAML index.
+struct Closest {
+    double t;
+    int id;
+    int nhit;
+    bool nan;
+};
+__device__ __forceinline__ void closest_init(Closest &c) { c.t = 0.0; c.id = -1; c.nhit = 0; c.nan = false; }
+__device__ __forceinline__ void closest_add(Closest &c, double t, int id) {
+    c.nhit++;
+    if (t != t) c.nan = true;
+    if (c.id < 0 || t < c.t || (t == c.t && id < c.id)) { c.t = t; c.id = id; }
+}
+
+// Sphere tail after the opp <= r2 test (bodies.rs:105-119).
+__device__ __forceinline__ bool sphere_tail(double r2, double opp, double adj, double &t) {
+    double th = sqrt(r2 - opp);
+    double d0 = adj - th, d1 = adj + th;
+    if (d0 < 0.0 && d1 < 0.0) return false;
+    t = d0 < 0.0 ? d1 : (d1 < 0.0 ? d0 : fmin(d0, d1));
+    return true;
+}
+
+struct Ray {
+    V3 o, d;
+};
+
+// AABB slab test (bodies.rs:242-282).  inv = 1/d, sg = (inv < 0).
+__device__ __forceinline__ bool aabb_hit(const RgBox &b, V3 o, V3 inv, int sx, int sy, int sz, double &t) {
+    double tmin = ((sx ? b.hi[0] : b.lo[0]) - o.x) * inv.x;
+    double tmax = ((sx ? b.lo[0] : b.hi[0]) - o.x) * inv.x;
+    double tymin = ((sy ? b.hi[1] : b.lo[1]) - o.y) * inv.y;
+    double tymax = ((sy ? b.lo[1] : b.hi[1]) - o.y) * inv.y;
+    if (tmin > tymax || tymin > tmax) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    double tzmin = ((sz ? b.hi[2] : b.lo[2]) - o.z) * inv.z;
+    double tzmax = ((sz ? b.lo[2] : b.hi[2]) - o.z) * inv.z;
+    if (tmin > tzmax || tzmin > tmax) return false;
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    if (tmin >= 0.0) { t = tmin; return true; }
+    if (tmax >= 0.0) { t = tmax; return true; }
+    return false;
+}
+
+// Disk (bodies.rs:173-192).
+__device__ __forceinline__ bool disk_hit(const RgDsk &k, V3 o, V3 d, double &t) {
+    double den = (k.nx * d.x + k.ny * d.y) + k.nz * d.z;
+    if (!(den > 1e-6)) return false;
+    V3 v = v3(k.ox - o.x, k.oy - o.y, k.oz - o.z);
+    double dist = ((v.x * k.nx + v.y * k.ny) + v.z * k.nz) / den;
+    if (!(dist >= 0.0)) return false;
+    V3 h = add(o, scl(d, dist));
+    V3 w = v3(h.x - k.ox, h.y - k.oy, h.z - k.oz);
+    if (!(sqrt(dot(w, w)) < k.r)) return false;
+    t = dist;
+    return true;
+}
+
+// Primary rays start at the origin (ray.rs:53), so c - o == c exactly and the
+// sphere's h.h and the plane's v.n are per-body constants (bit-identical to
+// the reference's per-ray values).  8 FP64 ops per sphere instead of 16.
+__device__ __forceinline__ void trace_primary(const RgKernelArgs &a, V3 d, Closest &c) {
+    for (int i = 0; i < a.n_sph; ++i) {
+        const RgSph s = rg_cptr(a.sph)[i];
+        const double cc = rg_cptr(a.sph_cc)[i];
+        double adj = (s.cx * d.x + s.cy * d.y) + s.cz * d.z;
+        double opp = cc - adj * adj;
+        if (!(opp > s.r2)) {
+            double t;
+            if (sphere_tail(s.r2, opp, adj, t)) closest_add(c, t, rg_cptr(a.sph_id)[i]);
+        }
+    }
+    for (int i = 0; i < a.n_pln; ++i) {
+        const RgPln p = rg_cptr(a.pln)[i];
+        double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;
+        if (den > 1e-6) {
+            double dist = p.on / den;
+            if (dist >= 0.0) closest_add(c, dist, rg_cptr(a.pln_id)[i]);
+        }
+    }
+    const V3 o = v3(0.0, 0.0, 0.0);
+    for (int i = 0; i < a.n_dsk; ++i) {
+        const RgDsk k = rg_cptr(a.dsk)[i];
+        double t;
+        if (disk_hit(k, o, d, t)) closest_add(c, t, rg_cptr(a.dsk_id)[i]);
+    }
+    if (a.n_box > 0) {
+        V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+        int sx = inv.x < 0.0, sy = inv.y < 0.0, sz = inv.z < 0.0;
+        for (int i = 0; i < a.n_box; ++i) {
+            const RgBox b = rg_cptr(a.box)[i];
+            double t;
+            if (aabb_hit(b, o, inv, sx, sy, sz, t)) closest_add(c, t, rg_cptr(a.box_id)[i]);
+        }
+    }
+}
+
+// General query: closest-hit for secondary rays, any-hit for shadow rays.
+// A shadow ray is occluded iff some body has a hit distance t with
+// !(t > light_distance)  <=>  !(min t > light_distance)  (rendering.rs:152-155),
+// so a lane stops testing at its first such hit and the wave leaves the body
+// loop as soon as every lane that is still testing is a finished shadow ray.
+__device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Ray &r, bool shadow, double ld,
+                                            Closest &c, bool &occl) {
+    const V3 o = r.o, d = r.d;
+    bool need = true;
+    for (int i = 0; i < a.n_sph; ++i) {
+        const RgSph s = rg_cptr(a.sph)[i];
+        double hx = s.cx - o.x, hy = s.cy - o.y, hz = s.cz - o.z;
+        double adj = (hx * d.x + hy * d.y) + hz * d.z;
+        double opp = ((hx * hx + hy * hy) + hz * hz) - adj * adj;
+        if (!(opp > s.r2) && need) {
+            double t;
+            if (sphere_tail(s.r2, opp, adj, t)) {
+                if (shadow) {
+                    if (!(t > ld)) { occl = true; need = false; }
+                } else {
+                    closest_add(c, t, rg_cptr(a.sph_id)[i]);
+                }
+            }
+        }
+        if ((i & 7) == 7 && !__any(need)) return;
+    }
+    if (!__any(need)) return;
+    for (int i = 0; i < a.n_pln; ++i) {
+        const RgPln p = rg_cptr(a.pln)[i];
+        double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;
+        if (den > 1e-6 && need) {
+            double vx = p.ox - o.x, vy = p.oy - o.y, vz = p.oz - o.z;
+            double dist = ((vx * p.nx + vy * p.ny) + vz * p.nz) / den;
+            if (dist >= 0.0) {
+                if (shadow) {
+                    if (!(dist > ld)) { occl = true; need = false; }
+                } else {
+                    closest_add(c, dist, rg_cptr(a.pln_id)[i]);
+                }
+            }
+        }
+    }
+    if (!__any(need)) return;
+    for (int i = 0; i < a.n_dsk; ++i) {
+        const RgDsk k = rg_cptr(a.dsk)[i];
+        double t;
+        if (need && disk_hit(k, o, d, t)) {
+            if (shadow) {
+                if (!(t > ld)) { occl = true; need = false; }
+            } else {
+                closest_add(c, t, rg_cptr(a.dsk_id)[i]);
+            }
+        }
+    }
+    if (a.n_box > 0 && __any(need)) {
+        V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+        int sx = inv.x < 0.0, sy = inv.y < 0.0, sz = inv.z < 0.0;
+        for (int i = 0; i < a.n_box; ++i) {
+            const RgBox b = rg_cptr(a.box)[i];
+            double t;
+            if (need && aabb_hit(b, o, inv, sx, sy, sz, t)) {
+                if (shadow) {
+                    if (!(t > ld)) { occl = true; need = false; }
+                } else {
+                    closest_add(c, t, rg_cptr(a.box_id)[i]);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- shading
+__device__ __forceinline__ V3 bp3(const RgBodyDev &b, int k) { return v3(b.p[k], b.p[k + 1], b.p[k + 2]); }
+
+// bodies.rs:122-124, 151-153, 194-196, 284-328.  false = the AABB assert.
+__device__ __forceinline__ bool surface_normal(const RgBodyDev &b, V3 h, V3 &n) {
+    if (b.kind == RG_BODY_SPHERE) { n = normalize(sub(h, bp3(b, 0))); return true; }
+    if (b.kind != RG_BODY_AABB) { n = neg(bp3(b, 3)); return true; }
+    if (fabs(h.x - b.p[0]) < 1e-8) n = v3(-1.0, 0.0, 0.0);
+    else if (fabs(h.x - b.p[3]) < 1e-8) n = v3(1.0, 0.0, 0.0);
+    else if (fabs(h.y - b.p[1]) < 1e-8) n = v3(0.0, -1.0, 0.0);
+    else if (fabs(h.y - b.p[4]) < 1e-8) n = v3(0.0, 1.0, 0.0);
+    else if (fabs(h.z - b.p[2]) < 1e-8) n = v3(0.0, 0.0, -1.0);
+    else if (fabs(h.z - b.p[5]) < 1e-8) n = v3(0.0, 0.0, 1.0);
+    else { n = v3(1.0, 0.0, 0.0); return false; }
+    return true;
+}
+
+// bodies.rs:126-132, 155-169, 198-212, 330-333
+__device__ __forceinline__ void texture_coords(const RgBodyDev &b, V3 h, float &tx, float &ty) {
+    if (b.kind == RG_BODY_SPHERE) {
+        V3 hv = sub(h, bp3(b, 0));
+        tx = (1.0f + ((float)atan2(hv.z, hv.x)) / PI_F) * 0.5f;
+        ty = ((float)acos(hv.y / b.p[3])) / PI_F;
+    } else if (b.kind == RG_BODY_AABB) {
+        tx = 0.0f;
+        ty = 0.0f;
+    } else {
+        V3 n = bp3(b, 3);
+        V3 xa = cross(n, v3(0.0, 0.0, 1.0));
+        if (dot(xa, xa) == 0.0) xa = cross(n, v3(0.0, 1.0, 0.0));
+        V3 ya = cross(n, xa);
+        V3 hv = sub(h, bp3(b, 0));
+        tx = (float)dot(hv, xa);
+        ty = (float)dot(hv, ya);
+    }
+}
+
+// material.rs:129-138
+__device__ __forceinline__ uint32_t wrap(float v, int32_t max) {
+    int32_t w = f32_to_i32(v * (float)max) % max;
+    return w < 0 ? (uint32_t)(w + max) : (uint32_t)w;
+}
+
+// material.rs:115-148 + color.rs:26-30
+__device__ __forceinline__ C3 material_color(const RgKernelArgs &a, const RgMatDev &m, float tx, float ty) {
+    if (m.coloration == RG_COLORATION_COLOR) return c3(m.color[0], m.color[1], m.color[2]);
+    const RgTexDev t = a.texs[m.tex];
+    uint32_t x = wrap(tx + m.xoff, t.w);
+    uint32_t y = wrap(ty + m.yoff, t.h);
+    uint32_t px = t.texels[(size_t)y * (uint32_t)t.w + x];
+    return c3((float)(px & 0xffu) / 255.0f, (float)((px >> 8) & 0xffu) / 255.0f,
+              (float)((px >> 16) & 0xffu) / 255.0f);
+}
+
+// rendering.rs:174-200, `cos_i = cos_t.abs()` (:194) kept as written.
+__device__ __forceinline__ double fresnel(V3 inc, V3 n, float index) {
+    double i_dot_n = dot(inc, n);
+    double eta_i, eta_t;
+    if (i_dot_n > 0.0) { eta_i = (double)index; eta_t = 1.0; }
+    else { eta_i = 1.0; eta_t = (double)index; }
+    double sin_t = eta_i / eta_t * sqrt(fmax(1.0 - i_dot_n * i_dot_n, 0.0));
+    if (sin_t > 1.0) return 1.0;
+    double cos_t = sqrt(fmax(1.0 - sin_t * sin_t, 0.0));
+    double cos_i = fabs(cos_t);
+    double r_s = ((eta_t * cos_i) - (eta_i * cos_t)) / ((eta_t * cos_i) + (eta_i * cos_t));
+    double r_p = ((eta_i * cos_i) - (eta_t * cos_t)) / ((eta_i * cos_i) + (eta_t * cos_t));
+    return (r_s * r_s + r_p * r_p) / 2.0;
+}
+
+// ray.rs:56-60
+__device__ __forceinline__ Ray reflection(V3 n, V3 inc, V3 h) {
+    Ray r;
+    r.o = add(h, scl(n, SHADOW_BIAS));
+    r.d = sub(inc, scl(n, 2.0 * dot(inc, n)));
+    return r;
+}
+
+// ray.rs:62-94
+__device__ __forceinline__ bool transmission(V3 n, V3 inc, V3 h, float index, Ray &r) {
+    V3 ref_n = n;
+    double eta_t = (double)index, eta_i = 1.0;
+    double i_dot_n = dot(inc, n);
+    if (i_dot_n < 0.0) i_dot_n = -i_dot_n;
+    else { ref_n = neg(n); eta_t = 1.0; eta_i = (double)index; }
+    double eta = eta_i / eta_t;
+    double k = 1.0 - (eta * eta) * (1.0 - i_dot_n * i_dot_n);
+    if (k < 0.0) return false;
+    r.o = add(h, scl(ref_n, -SHADOW_BIAS));
+    r.d = sub(scl(add(inc, scl(ref_n, i_dot_n)), eta), scl(ref_n, sqrt(k)));
+    return true;
+}
+
+// lights.rs:46-58
+__device__ __forceinline__ V3 light_dir(const RgLightDev &l, V3 p) {
+    if (l.kind == RG_LIGHT_DIRECTIONAL) return normalize(neg(v3(l.v[0], l.v[1], l.v[2])));
+    return normalize(sub(v3(l.v[0], l.v[1], l.v[2]), p));
+}
+__device__ __forceinline__ double light_distance(const RgLightDev &l, V3 p) {
+    if (l.kind == RG_LIGHT_DIRECTIONAL) return __builtin_inf();
+    V3 d = sub(v3(l.v[0], l.v[1], l.v[2]), p);
+    return sqrt(dot(d, d));
+}
+__device__ __forceinline__ float light_intensity(const RgLightDev &l, V3 p) {  // lights.rs:36-44
+    if (l.kind == RG_LIGHT_DIRECTIONAL) return l.intensity;
+    V3 d = sub(v3(l.v[0], l.v[1], l.v[2]), p);
+    float r2 = (float)dot(d, d);
+    return l.intensity / (4.0f * PI_F * r2);
+}
+
+// One open node of the shading tree.
+struct Frame {
+    float f[8];   // REFL: D.rgb, r.  REFR: kr, tau, surf.rgb, Tc.rgb
+    double rr[6]; // REFR_T: pending reflection ray (origin, direction)
+    int type;
+    int cdepth;   // depth of this node's children
+};
+
+__device__ __forceinline__ uint32_t out_row_to_y(const RgKernelArgs &a, uint32_t orow) {
+    uint32_t tl = orow / a.tile_rows, r = orow - tl * a.tile_rows;
+    unsigned long long y = ((unsigned long long)tl * a.tile_stride + a.tile_offset) * a.tile_rows + r;
+    return y >= a.height ? 0xFFFFFFFFu : (uint32_t)y;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+}  // namespace rgk
+
+using namespace rgk;
+
+template <int MAXD>
+__global__ __launch_bounds__(256) void rg_render_kernel(RgKernelArgs a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t x = blockIdx.x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
+    const uint32_t orow = blockIdx.y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
+    bool alive = x < a.width && orow < a.out_rows;
+    uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
+    const size_t oidx = (size_t)orow * a.width + x;
+    if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
+        a.rgba[oidx] = 0u;
+        if (a.rgb) { a.rgb[3 * oidx] = 0.0f; a.rgb[3 * oidx + 1] = 0.0f; a.rgb[3 * oidx + 2] = 0.0f; }
+        alive = false;
+    }
+    const uint32_t pixel = y * a.width + x;
+    const C3 def = c3(a.def[0], a.def[1], a.def[2]);
+    const int max_depth = (int)a.max_depth;
+
+    unsigned long long n_prim = 0, n_shadow = 0, n_sec = 0;
+
+    int mode = MODE_DONE;
+    Ray q;                 // current query
+    double ld = 0.0;       // shadow: light distance
+    int qdepth = 0;        // closest: depth of the ray
+    // hit being shaded
+    V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0), hd = v3(0, 0, 0);
+    int hb = 0, hdepth = 0, li = 0;
+    C3 fin = c3(0, 0, 0), bcol = c3(0, 0, 0), ret = def;
+    Frame stk[MAXD];
+    int sp = 0;
+    Closest c;
+    closest_init(c);
+
+    if (alive) {
+        // ray.rs:37-54 (aspect and fov_adjustment are per-frame constants)
+        double sx = ((((double)x + 0.5) / (double)a.width) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
+        double sy = (1.0 - (((double)y + 0.5) / (double)a.height) * 2.0) * a.fov_adjustment;
+        q.o = v3(0.0, 0.0, 0.0);
+        q.d = normalize(v3(sx, sy, -1.0));
+        n_prim = 1;
+        trace_primary(a, q.d, c);
+        mode = MODE_CLOSEST;
+        qdepth = 0;
+    }
+
+    bool have_result = alive;  // c / occl hold a fresh result for the lane's query
+    bool occl = false;
+    for (;;) {
+        if (have_result) {
+            bool unwind = false;
+            bool shade = false;           // run a shade_diffuse step this iteration
+            const int rmode = mode;       // kind of result the lane holds
+            if (rmode == MODE_CLOSEST) {
+                if (c.nan && c.nhit >= 2) raise_error(a, pixel, RG_ERR_NAN_DISTANCE);
+                if (c.id < 0) {
+                    ret = def;  // rendering.rs:76-77, 128-129
+                    unwind = true;
+                } else {
+                    // get_color (rendering.rs:80-120)
+                    const RgBodyDev b = a.bodies[c.id];
+                    const RgMatDev m = a.mats[c.id];
+                    V3 h = add(q.o, scl(q.d, c.t));
+                    V3 n;
+                    if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
+                    if (m.surface != RG_SURFACE_REFRACTIVE) {
+                        float tx, ty;
+                        texture_coords(b, h, tx, ty);
+                        bcol = material_color(a, m, tx, ty);
+                        fin = c3(0.0f, 0.0f, 0.0f);
+                        hp = h; hn = n; hd = q.d; hb = c.id; hdepth = qdepth; li = 0;
+                        shade = true;
+                    } else {
+                        float kr = (float)fresnel(q.d, n, m.index);
+                        float tx, ty;
+                        texture_coords(b, h, tx, ty);
+                        C3 surf = material_color(a, m, tx, ty);
+                        Ray rr = reflection(n, q.d, h);
+                        int cd = qdepth + 1;
+                        C3 tc = def;
+                        bool trace_t = false;
+                        Ray tr;
+                        if (kr < 1.0f) {
+                            if (!transmission(n, q.d, h, m.index, tr)) raise_error(a, pixel, RG_ERR_TRANSMISSION);
+                            else if (cd < max_depth) trace_t = true;
+                        }
+                        if (cd >= max_depth) {
+                            C3 col = cadd(cscl(def, kr), cscl(tc, 1.0f - kr));
+                            ret = cmul(cscl(col, m.transparency), surf);
+                            unwind = true;
+                        } else {
+                            Frame &f = stk[sp++];
+                            f.f[0] = kr; f.f[1] = m.transparency;
+                            f.f[2] = surf.r; f.f[3] = surf.g; f.f[4] = surf.b;
+                            f.f[5] = tc.r; f.f[6] = tc.g; f.f[7] = tc.b;
+                            f.cdepth = cd;
+                            if (trace_t) {
+                                f.type = FR_REFR_T;
+                                f.rr[0] = rr.o.x; f.rr[1] = rr.o.y; f.rr[2] = rr.o.z;
+                                f.rr[3] = rr.d.x; f.rr[4] = rr.d.y; f.rr[5] = rr.d.z;
+                                q = tr;
+                            } else {
+                                f.type = FR_REFR_R;
+                                q = rr;
+                            }
+                            qdepth = cd;
+                            mode = MODE_CLOSEST;
+                            n_sec++;
+                        }
+                    }
+                }
+            } else {
+                shade = true;  // a shadow result for light li
+            }
+            if (shade) {
+                // shade_diffuse loop body (rendering.rs:141-170)
+                const RgMatDev m = a.mats[hb];
+                if (rmode == MODE_SHADOW) {
+                    const RgLightDev l = rg_cptr(a.lights)[li];
+                    float inten = !occl ? light_intensity(l, hp) : 0.0f;
+                    float power = fmaxf((float)dot(hn, q.d), 0.0f) * inten;
+                    float refl = m.albedo / PI_F;
+                    C3 lc = cscl(cscl(c3(l.color[0], l.color[1], l.color[2]), power), refl);
+                    fin = cadd(fin, cmul(bcol, lc));
+                    li++;
+                }
+                if (li < a.n_lights) {
+                    const RgLightDev l = rg_cptr(a.lights)[li];
+                    q.o = add(hp, scl(hn, SHADOW_BIAS));
+                    q.d = light_dir(l, hp);
+                    ld = light_distance(l, hp);
+                    mode = MODE_SHADOW;
+                    n_shadow++;
+                } else {
+                    C3 dcol = cclamp(fin);
+                    if (m.surface == RG_SURFACE_DIFFUSE) {
+                        ret = dcol;
+                        unwind = true;
+                    } else {  // Reflecting (rendering.rs:86-91)
+                        float r = m.reflectivity;
+                        int cd = hdepth + 1;
+                        if (cd >= max_depth) {
+                            ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
+                            unwind = true;
+                        } else {
+                            Frame &f = stk[sp++];
+                            f.type = FR_REFL;
+                            f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = r;
+                            f.cdepth = cd;
+                            q = reflection(hn, hd, hp);
+                            qdepth = cd;
+                            mode = MODE_CLOSEST;
+                            n_sec++;
+                        }
+                    }
+                }
+            }
+            if (unwind) {
+                for (;;) {
+                    if (sp == 0) {
+                        a.rgba[oidx] = f32_to_u8(ret.r * 255.0f) | (f32_to_u8(ret.g * 255.0f) << 8) |
+                                       (f32_to_u8(ret.b * 255.0f) << 16) | 0xFF000000u;
+                        if (a.rgb) { a.rgb[3 * oidx] = ret.r; a.rgb[3 * oidx + 1] = ret.g; a.rgb[3 * oidx + 2] = ret.b; }
+                        mode = MODE_DONE;
+                        break;
+                    }
+                    Frame &f = stk[sp - 1];
+                    if (f.type == FR_REFL) {
+                        ret = cadd(cscl(c3(f.f[0], f.f[1], f.f[2]), 1.0f - f.f[3]), cscl(ret, f.f[3]));
+                        sp--;
+                    } else if (f.type == FR_REFR_T) {
+                        f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
+                        f.type = FR_REFR_R;
+                        q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
+                        q.d = v3(f.rr[3], f.rr[4], f.rr[5]);
+                        qdepth = f.cdepth;
+                        mode = MODE_CLOSEST;
+                        n_sec++;
+                        break;
+                    } else {  // FR_REFR_R (rendering.rs:115-117)
+                        float kr = f.f[0];
+                        C3 col = cadd(cscl(ret, kr), cscl(c3(f.f[5], f.f[6], f.f[7]), 1.0f - kr));
+                        ret = cmul(cscl(col, f.f[1]), c3(f.f[2], f.f[3], f.f[4]));
+                        sp--;
+                    }
+                }
+            }
+        }
+        const bool live = mode != MODE_DONE;
+        if (!__any(live)) break;
+        if (live) {
+            closest_init(c);
+            occl = false;
+            trace_query(a, q, mode == MODE_SHADOW, ld, c, occl);
+        }
+        have_result = live;
+    }
+
+    // ray counters: wave reduction, one atomic per wave per class
+    n_prim = wave_sum(n_prim);
+    n_shadow = wave_sum(n_shadow);
+    n_sec = wave_sum(n_sec);
+    if (lane == 0) {
+        if (n_prim) atomicAdd(&a.counters[0], n_prim);
+        if (n_shadow) atomicAdd(&a.counters[1], n_shadow);
+        if (n_sec) atomicAdd(&a.counters[2], n_sec);
+    }
+}
+
+// Scene::trace for a batch of rays (rg_trace): one lane per ray.
+__global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const double *rays, uint32_t n,
+                                                       double *dist, int32_t *body) {
+    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    bool alive = i < n;
+    Ray r;
+    r.o = v3(0, 0, 0);
+    r.d = v3(0, 0, 1);
+    if (alive) {
+        r.o = v3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+        r.d = v3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+    }
+    Closest c;
+    closest_init(c);
+    bool occl = false;
+    if (alive) {
+        trace_query(a, r, false, 0.0, c, occl);
+        if (c.nan && c.nhit >= 2) raise_error(a, i, RG_ERR_NAN_DISTANCE);
+        dist[i] = c.id >= 0 ? c.t : 0.0;
+        body[i] = c.id;
+    }
+}
+
+// ---------------------------------------------------------------- launchers
+extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {
+    dim3 grid((a->width + 15) / 16, (a->out_rows + 15) / 16);
+    dim3 block(256);
+    if (maxd <= 8) hipLaunchKernelGGL(rg_render_kernel<8>, grid, block, 0, stream, *a);
+    else if (maxd <= 16) hipLaunchKernelGGL(rg_render_kernel<16>, grid, block, 0, stream, *a);
+    else if (maxd <= 64) hipLaunchKernelGGL(rg_render_kernel<64>, grid, block, 0, stream, *a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,
+                                      int32_t *body, hipStream_t stream) {
+    dim3 grid((n + 255) / 256);
+    hipLaunchKernelGGL(rg_trace_kernel, grid, dim3(256), 0, stream, *a, rays, n, dist, body);
+    return hipGetLastError();
+}
