@@ -1,0 +1,284 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s of the per-pixel ray-trace path (BASELINE.json metric).
+
+One step = one frame of the workload rendered by the HIP megakernel, scene and
+textures already resident in HBM, framebuffer left in HBM (rank 0 holds the
+assembled frame).  At N>1 (torchrun, one rank per GPU) the frame is cut into
+16-row tiles dealt round-robin to the ranks and the tiles are gathered to rank
+0 with one RCCL gather (torch.distributed backend "nccl" = RCCL over xGMI),
+then re-interleaved into image order on rank 0.
+
+Workload (BASELINE.json configs[1]): examples/test1.yml at 3840x2160,
+recursion depth 5, 1 GPU.  `--workload synth1024` selects the north_star's
+1024-sphere 3840x2160 depth-5 scene instead.
+
+Prints ONE JSON line on rank 0 (the driver's contract) with `roofline`
+(FP64-VALU bound, from HIP events on the render stream), `roofline_hbm`
+(achieved HBM bytes, as the north_star asks) and `cpu_baseline` (the CPU
+restatement in oracle/, timed on this host's cores on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+METRIC = "Mrays/sec (primary+shadow+secondary) at 3840×2160, depth 5; 1/2/4/8 MI355X"
+FP64_PEAK_TOPS = 39.3     # MI355X FP64 vector 78.6 TFLOP/s spec counts FMA as 2; parity forbids FMA -> 39.3 T ops/s
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+# Algorithmic FP64 ops per body test on the reference's miss path.
+OPS_PER_BODY = {"sphere": 16, "plane": 14, "disk": 20, "aabb": 18}
+TILE_ROWS = 16
+
+
+def load_workload(name: str):
+    from raingun_amd.scene import AABB, Disk, Plane, Sphere, load_scene
+    from raingun_amd.synth import scene_md5, synthetic_yaml
+
+    golden = REPO / "tests" / "golden"
+    if name == "test1":
+        scene = load_scene(golden / "examples" / "test1.yml", texture_root=golden)
+        scene.max_recursion_depth = 5
+        label = "examples/test1.yml 3840x2160 depth 5 (BASELINE configs[1])"
+        src = "reference example scene examples/test1.yml; textures decoded on the host (PIL)"
+    elif name == "test3":
+        scene = load_scene(golden / "examples" / "test3.yml", texture_root=golden)
+        label = "examples/test3.yml 3840x2160 depth 10 (BASELINE configs[2])"
+        src = "reference example scene examples/test3.yml; textures decoded on the host (PIL)"
+    elif name.startswith("synth"):
+        n = int(name[5:] or 1024)
+        text = synthetic_yaml(n, 2, 5)
+        scene = load_scene(text)
+        label = f"synthetic {n} spheres + 2 planes 3840x2160 depth 5 (seed 0x5EED, md5 {scene_md5(text)})"
+        src = "synthetic seeded scene (raingun_amd/synth.py)"
+    else:
+        raise SystemExit(f"unknown workload {name}")
+    counts = {"sphere": 0, "plane": 0, "disk": 0, "aabb": 0}
+    for b in scene.bodies:
+        counts[{Sphere: "sphere", Plane: "plane", Disk: "disk", AABB: "aabb"}[type(b)]] += 1
+    ops_per_ray = sum(OPS_PER_BODY[k] * v for k, v in counts.items())
+    return scene, label, src, counts, ops_per_ray
+
+
+def texture_bytes(scene) -> int:
+    from raingun_amd.scene import Texture
+
+    seen, total = set(), 0
+    for b in scene.bodies:
+        c = b.material.coloration
+        if isinstance(c, Texture) and id(c.image) not in seen:
+            seen.add(id(c.image))
+            total += c.image.size
+    return total
+
+
+def cpu_baseline(scene, width, height, budget_s: float = 12.0):
+    """CPU restatement (oracle/) on this host's cores, on a bounded sample of the
+    same frame: every k-th 16-row tile, k grown until one pass fits the budget."""
+    import oracle
+    from raingun_amd.scene import SceneDesc
+
+    desc = SceneDesc(scene)
+    threads = oracle.default_threads()
+    tiles = (height + TILE_ROWS - 1) // TILE_ROWS
+    stride = 1  # first probe: the whole frame
+    while True:
+        t0 = time.perf_counter()
+        st, _, _, counts, _ = oracle.render(desc, width, height, TILE_ROWS, stride, 0, threads=threads)
+        dt = time.perf_counter() - t0
+        if st != 0:
+            raise RuntimeError(f"oracle status {st}")
+        if dt * stride <= budget_s or stride >= tiles:
+            break
+        stride = min(tiles, int(stride * (dt * stride / budget_s)) + 1)
+    reps, elapsed, rays = 1, dt, sum(counts.values())
+    while elapsed < budget_s / 2 and reps < 100:
+        t0 = time.perf_counter()
+        oracle.render(desc, width, height, TILE_ROWS, stride, 0, threads=threads)
+        elapsed += time.perf_counter() - t0
+        reps += 1
+    rows = oracle.lib().rgo_tiling_rows(height, __import__("raingun_amd")._abi.rg_tiling(TILE_ROWS, stride, 0))
+    return {
+        "value": round(rays * reps / elapsed / 1e6, 3),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"every {stride}th 16-row tile of the same frame ({min(rows, height)} of {height} rows, "
+                  f"{rays} rays) x{reps} passes, {elapsed:.1f}s; CPU restatement oracle/raingun_oracle.c, "
+                  f"-O2 -ffp-contract=off, {threads} pthreads",
+    }
+
+
+def load_traffic(workload: str, n_gpus: int):
+    f = REPO / "profiles" / "traffic.json"
+    if n_gpus != 1 or not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get(workload, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="test1", help="test1 | test3 | synth<N>")
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from raingun_amd import _abi
+    from raingun_amd.scene import DeviceScene
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local_rank)
+
+    scene, label, src, body_counts, ops_per_ray = load_workload(args.workload)
+    W, H = args.width, args.height
+    ds = DeviceScene(scene, device=local_rank)  # scene + textures uploaded once, resident in HBM
+    lib = _abi.lib()
+
+    tiles = (H + TILE_ROWS - 1) // TILE_ROWS
+    tiles_per_rank = (tiles + world - 1) // world
+    tiling = _abi.rg_tiling(TILE_ROWS, world, rank)
+    my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
+    slot_rows = tiles_per_rank * TILE_ROWS  # equal-size gather slots (last ranks zero-padded)
+    out = torch.zeros((slot_rows, W, 4), dtype=torch.uint8, device=dev)
+    gathered = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    frame = torch.empty((tiles * TILE_ROWS, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
+
+    stream = torch.cuda.current_stream(dev)
+    sh = C.c_void_p(stream.cuda_stream)
+
+    def render(stats=None):
+        st = lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(out.data_ptr()), None, sh,
+                                       C.byref(stats) if stats is not None else None)
+        _abi.check(st, "rg_render_tiles_async")
+
+    def assemble():
+        if world == 1:
+            return
+        dist.gather(out, gathered, dst=0)
+        if rank == 0:
+            g = torch.stack(gathered)  # (ranks, tiles_per_rank, T, W, 4): tile j*world + r <- g[r, j]
+            g = g.view(world, tiles_per_rank, TILE_ROWS, W, 4).transpose(0, 1).reshape(-1, W, 4)
+            frame.copy_(g[:tiles * TILE_ROWS])
+
+    # one counted render: ray totals per class (deterministic per frame)
+    stats = _abi.rg_stats()
+    render(stats)
+    rays = torch.tensor([stats.rays.primary, stats.rays.shadow, stats.rays.secondary], dtype=torch.float64,
+                        device=dev)
+    if world > 1:
+        dist.all_reduce(rays)
+    rays = [int(x) for x in rays.tolist()]
+    rays_per_frame = sum(rays)
+
+    for _ in range(args.warmup):
+        render()
+        assemble()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        render()
+        ev[i][1].record(stream)
+        assemble()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms_max = float(tt[0]), float(tt[1])
+
+    if rank == 0:
+        ms_per_step = elapsed * 1e3 / args.steps
+        value = rays_per_frame * args.steps / elapsed / 1e6
+        # roofline of the dominant kernel (rg_render_kernel) on this rank
+        my_rays = stats.rays.primary + stats.rays.shadow + stats.rays.secondary
+        ops = my_rays * ops_per_ray
+        achieved_t = ops / (kernel_ms * 1e-3) / 1e12
+        out_bytes = my_rows * W * 4
+        tex = texture_bytes(scene)
+        alg_bytes = out_bytes  # framebuffer written once; scene/texture reads are cache-resident re-reads
+        traffic = load_traffic(args.workload, world)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": src,
+            "config": {"workload": label, "width": W, "height": H, "max_recursion_depth": scene.max_recursion_depth,
+                       "bodies": body_counts, "lights": len(scene.lights), "tile_rows": TILE_ROWS,
+                       "parallelism": f"row-tiles x{world} (round-robin 16-row tiles, RCCL gather to rank 0)"},
+            "rays_per_frame": {"primary": rays[0], "shadow": rays[1], "secondary": rays[2], "total": rays_per_frame},
+            "kernel_ms": round(kernel_ms, 4),
+            "roofline": {
+                "bound": "valu_fp64",
+                "achieved": round(achieved_t, 4),
+                "peak": FP64_PEAK_TOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved_t / FP64_PEAK_TOPS, 5),
+                "traffic": traffic,
+                "basis": f"{ops_per_ray} algorithmic FP64 ops per ray (16/sphere, 14/plane, 20/disk, 18/aabb) x "
+                         f"{my_rays} rays per launch / mean rg_render_kernel time from HIP events on the render stream",
+            },
+            "roofline_hbm": {
+                "bound": "hbm",
+                "achieved": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 3),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(alg_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),
+                "traffic": traffic,
+                "basis": f"{alg_bytes} B framebuffer written per launch (+{tex} B of textures, L2/MALL resident)",
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(scene, W, H)
+            line["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
+        print(json.dumps(line), flush=True)
+    ds.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

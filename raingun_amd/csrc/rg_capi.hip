@@ -309,8 +309,7 @@ rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t heig
     a.aspect = (double)width / (double)height;
     a.rgba = reinterpret_cast<uint32_t *>(rgba_dev);
     a.rgb = rgb_dev;
-    static const unsigned long long init[4] = {0, 0, 0, RG_ERRKEY_NONE};
-    if (!ok(hipMemcpyAsync(s->counters, init, sizeof init, hipMemcpyHostToDevice, st))) return RG_ERR_DEVICE;
+    if (!ok(hipMemsetAsync(s->counters, 0, 4 * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
     if (out_rows == 0) return RG_OK;
     if (stats && !ok(hipEventRecord(s->ev0, st))) return RG_ERR_DEVICE;
     if (!ok(rg_launch_render(&a, frames_needed(s->max_depth), st))) return RG_ERR_DEVICE;
@@ -326,9 +325,10 @@ rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t heig
     stats->rays.secondary = c[2];
     stats->kernel_ms = ms;
     stats->error_pixel = -1;
-    if (c[3] != RG_ERRKEY_NONE) {
-        stats->error_pixel = (int32_t)(c[3] >> 8);
-        return (rg_status)(-(int32_t)(c[3] & 0xff));
+    if (c[3] != 0) {
+        unsigned long long key = ~c[3];
+        stats->error_pixel = (int32_t)(key >> 8);
+        return (rg_status)(-(int32_t)(key & 0xff));
     }
     return RG_OK;
 }
@@ -436,10 +436,9 @@ rg_status rg_trace(const rg_scene *s, const double *rays, uint32_t n, double *di
         !ok(hipMalloc(&d_body, (size_t)n * 4)))
         st = RG_ERR_OUT_OF_MEMORY;
     RgKernelArgs a = make_args(s);
-    static const unsigned long long init[4] = {0, 0, 0, RG_ERRKEY_NONE};
-    unsigned long long c[4] = {0, 0, 0, RG_ERRKEY_NONE};
+    unsigned long long c[4] = {0, 0, 0, 0};
     if (st == RG_OK && (!ok(hipMemcpy(d_rays, rays, (size_t)n * 48, hipMemcpyHostToDevice)) ||
-                        !ok(hipMemcpy(s->counters, init, sizeof init, hipMemcpyHostToDevice)) ||
+                        !ok(hipMemset(s->counters, 0, sizeof c)) ||
                         !ok(rg_launch_trace(&a, (const double *)d_rays, n, (double *)d_dist, (int32_t *)d_body, nullptr)) ||
                         !ok(hipMemcpy(dist, d_dist, (size_t)n * 8, hipMemcpyDeviceToHost)) ||
                         !ok(hipMemcpy(body, d_body, (size_t)n * 4, hipMemcpyDeviceToHost)) ||
@@ -448,7 +447,7 @@ rg_status rg_trace(const rg_scene *s, const double *rays, uint32_t n, double *di
     if (d_rays) hipFree(d_rays);
     if (d_dist) hipFree(d_dist);
     if (d_body) hipFree(d_body);
-    if (st == RG_OK && c[3] != RG_ERRKEY_NONE) st = (rg_status)(-(int32_t)(c[3] & 0xff));
+    if (st == RG_OK && c[3] != 0) st = (rg_status)(-(int32_t)((~c[3]) & 0xff));
     return st;
 }
 

@@ -93,8 +93,8 @@ struct RgKernelArgs {
     // outputs
     uint32_t *rgba;          // packed RGBA8, out_rows * width
     float *rgb;              // nullable, out_rows * width * 3
-    unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=error key
+    unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=~error key
 };
 
-// error key: (pixel << 8) | (-status); atomicMin keeps the lowest pixel.
-#define RG_ERRKEY_NONE 0xFFFFFFFFFFFFFFFFull
+// counters[3] holds ~((pixel << 8) | -status) of the lowest erroring pixel
+// (atomicMax of the complement); 0 = no error, so one memset resets all four.

@@ -67,8 +67,9 @@ __device__ __forceinline__ int32_t f32_to_i32(float v) {
 }
 
 __device__ __forceinline__ void raise_error(const RgKernelArgs &a, uint32_t pixel, int status) {
+    // lowest pixel wins: max of the complemented key; 0 (memset) = no error
     unsigned long long key = ((unsigned long long)pixel << 8) | (unsigned long long)(-status);
-    atomicMin(&a.counters[3], key);
+    atomicMax(&a.counters[3], ~key);
 }
 
 // ---------------------------------------------------------------- closest hit
