@@ -159,31 +159,39 @@ def main() -> None:
     ds = DeviceScene(scene, device=local_rank)  # scene + textures uploaded once, resident in HBM
     lib = _abi.lib()
 
-    tiles = (H + TILE_ROWS - 1) // TILE_ROWS
-    tiles_per_rank = (tiles + world - 1) // world
-    tiling = _abi.rg_tiling(TILE_ROWS, world, rank)
+    from raingun_amd import distributed as rd
+
+    tiling = rd.tiling(rank, world, TILE_ROWS)
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
-    slot_rows = tiles_per_rank * TILE_ROWS  # equal-size gather slots (last ranks zero-padded)
-    out = torch.zeros((slot_rows, W, 4), dtype=torch.uint8, device=dev)
+    slot = rd.slot_rows(H, world, TILE_ROWS)  # equal-size gather slots (last ranks zero-padded)
+    out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
     gathered = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
-    frame = torch.empty((tiles * TILE_ROWS, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
+    frame = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
 
     stream = torch.cuda.current_stream(dev)
     sh = C.c_void_p(stream.cuda_stream)
+    events = []  # (start, end) around each timed launch, on the render stream
 
     def render(stats=None):
         st = lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(out.data_ptr()), None, sh,
                                        C.byref(stats) if stats is not None else None)
         _abi.check(st, "rg_render_tiles_async")
 
-    def assemble():
-        if world == 1:
-            return
-        dist.gather(out, gathered, dst=0)
-        if rank == 0:
-            g = torch.stack(gathered)  # (ranks, tiles_per_rank, T, W, 4): tile j*world + r <- g[r, j]
-            g = g.view(world, tiles_per_rank, TILE_ROWS, W, 4).transpose(0, 1).reshape(-1, W, 4)
-            frame.copy_(g[:tiles * TILE_ROWS])
+    def render_tiles(_t):
+        if events is not None and len(events) < max_events[0]:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            render()
+            b.record(stream)
+            events.append((a, b))
+        else:
+            render()
+        return out
+
+    max_events = [0]
+
+    def step():
+        rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
 
     # one counted render: ray totals per class (deterministic per frame)
     stats = _abi.rg_stats()
@@ -196,26 +204,22 @@ def main() -> None:
     rays_per_frame = sum(rays)
 
     for _ in range(args.warmup):
-        render()
-        assemble()
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    max_events[0] = args.steps
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        render()
-        ev[i][1].record(stream)
-        assemble()
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    kernel_ms = sum(a.elapsed_time(b) for a, b in events) / len(events)
 
     tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:

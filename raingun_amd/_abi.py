@@ -176,6 +176,14 @@ def lib() -> C.CDLL:
             raise RuntimeError(
                 f"{path} is missing: build it with `make -C raingun_amd/csrc` (or __graft_entry__.build()). "
                 "There is no CPU fallback for the render path.")
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64,
+        # which satisfies this library's libamdhip64.so.7 dependency when torch
+        # is imported first.  Loading /opt/rocm's runtime first would leave two
+        # runtimes in the process and torch would then see no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:  # pragma: no cover - torch is part of the image
+            pass
         lib_ = C.CDLL(path)
         _declare(lib_)
         _LIB = lib_

@@ -93,7 +93,7 @@ struct RgKernelArgs {
     // outputs
     uint32_t *rgba;          // packed RGBA8, out_rows * width
     float *rgb;              // nullable, out_rows * width * 3
-    unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=~error key
+    unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=~error key [4]=tile queue
 };
 
 // counters[3] holds ~((pixel << 8) | -status) of the lowest erroring pixel

@@ -18,6 +18,8 @@
 // Division and sqrt are the correctly-rounded hipcc expansions.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/raingun.h"
 #include "rg_device.h"
 
@@ -134,20 +136,93 @@ __device__ __forceinline__ bool disk_hit(const RgDsk &k, V3 o, V3 d, double &t) 
     return true;
 }
 
+// ---------------------------------------------------------------- sphere sources
+// The sphere tables are read with a wave-uniform index.  Two sources:
+//  * SphLds: the block stages the tables into LDS once (persistent blocks),
+//    then every test reads them with broadcast ds_read_b128 (always a hit,
+//    ~100-cycle latency hidden by prefetching the next record);
+//  * SphScalar: scalar loads through the constant address space (s_load,
+//    SGPR operands) for scenes whose tables exceed the LDS budget.
+struct SphScalar {
+    const RG_CONST RgSph *s;
+    const RG_CONST double *cc;
+    __device__ __forceinline__ RgSph get(int i) const { return s[i]; }
+    __device__ __forceinline__ double getcc(int i) const { return cc[i]; }
+};
+struct SphLds {
+    const RgSph *s;
+    const double *cc;
+    __device__ __forceinline__ RgSph get(int i) const { return s[i]; }
+    __device__ __forceinline__ double getcc(int i) const { return cc[i]; }
+};
+
+// primary rays (origin 0): adj = c.d, opp = (c.c) - adj*adj  (8 FP64 ops)
+__device__ __forceinline__ void sph_primary_one(const RgKernelArgs &a, int i, const RgSph &s, double cc, V3 d,
+                                                Closest &c) {
+    double adj = (s.cx * d.x + s.cy * d.y) + s.cz * d.z;
+    double opp = cc - adj * adj;
+    if (!(opp > s.r2)) {
+        double t;
+        if (sphere_tail(s.r2, opp, adj, t)) closest_add(c, t, rg_cptr(a.sph_id)[i]);
+    }
+}
+
+template <class Src>
+__device__ __forceinline__ void sph_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
+    const int n = a.n_sph;
+    if (n <= 0) return;
+    RgSph s = src.get(0);
+    double cc = src.getcc(0);
+    for (int i = 0; i < n; ++i) {
+        const int j = i + 1 < n ? i + 1 : i;  // prefetch the next record (clamped)
+        RgSph sn = src.get(j);
+        double ccn = src.getcc(j);
+        sph_primary_one(a, i, s, cc, d, c);
+        s = sn;
+        cc = ccn;
+    }
+}
+
+// general rays: closest-hit (secondary) or any-hit (shadow, see trace_query)
+__device__ __forceinline__ void sph_query_one(const RgKernelArgs &a, int i, const RgSph &s, V3 o, V3 d, bool shadow,
+                                              double ld, Closest &c, bool &occl, bool &need) {
+    double hx = s.cx - o.x, hy = s.cy - o.y, hz = s.cz - o.z;
+    double adj = (hx * d.x + hy * d.y) + hz * d.z;
+    double opp = ((hx * hx + hy * hy) + hz * hz) - adj * adj;
+    if (!(opp > s.r2) && need) {
+        double t;
+        if (sphere_tail(s.r2, opp, adj, t)) {
+            if (shadow) {
+                if (!(t > ld)) { occl = true; need = false; }
+            } else {
+                closest_add(c, t, rg_cptr(a.sph_id)[i]);
+            }
+        }
+    }
+}
+
+template <class Src>
+__device__ __forceinline__ bool sph_query(const RgKernelArgs &a, const Src &src, V3 o, V3 d, bool shadow, double ld,
+                                          Closest &c, bool &occl, bool &need) {
+    const int n = a.n_sph;
+    if (n <= 0) return true;
+    RgSph s = src.get(0);
+    for (int i = 0; i < n; ++i) {
+        const int j = i + 1 < n ? i + 1 : i;
+        RgSph sn = src.get(j);
+        sph_query_one(a, i, s, o, d, shadow, ld, c, occl, need);
+        s = sn;
+        if ((i & 7) == 7 && !__any(need)) return false;
+    }
+    return __any(need);
+}
+
 // Primary rays start at the origin (ray.rs:53), so c - o == c exactly and the
 // sphere's h.h and the plane's v.n are per-body constants (bit-identical to
 // the reference's per-ray values).  8 FP64 ops per sphere instead of 16.
-__device__ __forceinline__ void trace_primary(const RgKernelArgs &a, V3 d, Closest &c) {
-    for (int i = 0; i < a.n_sph; ++i) {
-        const RgSph s = rg_cptr(a.sph)[i];
-        const double cc = rg_cptr(a.sph_cc)[i];
-        double adj = (s.cx * d.x + s.cy * d.y) + s.cz * d.z;
-        double opp = cc - adj * adj;
-        if (!(opp > s.r2)) {
-            double t;
-            if (sphere_tail(s.r2, opp, adj, t)) closest_add(c, t, rg_cptr(a.sph_id)[i]);
-        }
-    }
+template <class Src>
+__device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
+    sph_primary(a, src, d, c);
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = rg_cptr(a.pln)[i];
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;
@@ -178,28 +253,12 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, V3 d, Close
 // !(t > light_distance)  <=>  !(min t > light_distance)  (rendering.rs:152-155),
 // so a lane stops testing at its first such hit and the wave leaves the body
 // loop as soon as every lane that is still testing is a finished shadow ray.
-__device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Ray &r, bool shadow, double ld,
+template <class Src>
+__device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &src, const Ray &r, bool shadow, double ld,
                                             Closest &c, bool &occl) {
     const V3 o = r.o, d = r.d;
     bool need = true;
-    for (int i = 0; i < a.n_sph; ++i) {
-        const RgSph s = rg_cptr(a.sph)[i];
-        double hx = s.cx - o.x, hy = s.cy - o.y, hz = s.cz - o.z;
-        double adj = (hx * d.x + hy * d.y) + hz * d.z;
-        double opp = ((hx * hx + hy * hy) + hz * hz) - adj * adj;
-        if (!(opp > s.r2) && need) {
-            double t;
-            if (sphere_tail(s.r2, opp, adj, t)) {
-                if (shadow) {
-                    if (!(t > ld)) { occl = true; need = false; }
-                } else {
-                    closest_add(c, t, rg_cptr(a.sph_id)[i]);
-                }
-            }
-        }
-        if ((i & 7) == 7 && !__any(need)) return;
-    }
-    if (!__any(need)) return;
+    if (!sph_query(a, src, o, d, shadow, ld, c, occl, need)) return;
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = rg_cptr(a.pln)[i];
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;
@@ -367,7 +426,8 @@ __device__ __forceinline__ uint32_t out_row_to_y(const RgKernelArgs &a, uint32_t
     return y >= a.height ? 0xFFFFFFFFu : (uint32_t)y;
 }
 
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+__device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
+    unsigned long long v = v32;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
 }
@@ -376,210 +436,243 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 
 using namespace rgk;
 
-template <int MAXD>
-__global__ __launch_bounds__(256) void rg_render_kernel(RgKernelArgs a) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t x = blockIdx.x * 16u + (uint32_t)((wave & 1) * 8 + (lane & 7));
-    const uint32_t orow = blockIdx.y * 16u + (uint32_t)((wave >> 1) * 8 + (lane >> 3));
-    bool alive = x < a.width && orow < a.out_rows;
-    uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
-    const size_t oidx = (size_t)orow * a.width + x;
-    if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
-        a.rgba[oidx] = 0u;
-        if (a.rgb) { a.rgb[3 * oidx] = 0.0f; a.rgb[3 * oidx + 1] = 0.0f; a.rgb[3 * oidx + 2] = 0.0f; }
-        alive = false;
+// Persistent render kernel.  Each wave repeatedly takes the next 8x8 pixel
+// tile from an atomic queue (counters[4]) and runs the per-lane state machine
+// until all 64 lanes have written their pixel.  With LDS, the block first
+// stages the sphere tables (RgSph[n], then cc[n]) into dynamic LDS.
+// MINW = minimum waves per SIMD requested from the register allocator:
+// 1 lets shading-heavy scenes keep everything in registers (2 waves/SIMD),
+// 4 caps the kernel at 128 VGPRs (cold shading state spills to scratch) so
+// body-heavy scenes get twice the waves to hide LDS/FP64 latency.
+template <int MAXD, bool LDS, int MINW>
+__global__ __launch_bounds__(256, MINW) void rg_render_kernel(RgKernelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    typename std::conditional<LDS, SphLds, SphScalar>::type src;
+    if constexpr (LDS) {
+        const int n = a.n_sph;
+        uint4 *dst = reinterpret_cast<uint4 *>(smem);
+        const uint4 *gs = reinterpret_cast<const uint4 *>(a.sph);
+        for (int k = threadIdx.x; k < n * 2; k += blockDim.x) dst[k] = gs[k];
+        double *dcc = reinterpret_cast<double *>(smem + (size_t)n * sizeof(RgSph));
+        for (int k = threadIdx.x; k < n; k += blockDim.x) dcc[k] = a.sph_cc[k];
+        __syncthreads();
+        src.s = reinterpret_cast<const RgSph *>(smem);
+        src.cc = dcc;
+    } else {
+        src.s = rg_cptr(a.sph);
+        src.cc = rg_cptr(a.sph_cc);
     }
-    const uint32_t pixel = y * a.width + x;
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t tiles_x = (a.width + 7u) / 8u;
+    const uint32_t ntiles = tiles_x * ((a.out_rows + 7u) / 8u);
     const C3 def = c3(a.def[0], a.def[1], a.def[2]);
     const int max_depth = (int)a.max_depth;
-
-    unsigned long long n_prim = 0, n_shadow = 0, n_sec = 0;
-
-    int mode = MODE_DONE;
-    Ray q;                 // current query
-    double ld = 0.0;       // shadow: light distance
-    int qdepth = 0;        // closest: depth of the ray
-    // hit being shaded
-    V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0), hd = v3(0, 0, 0);
-    int hb = 0, hdepth = 0, li = 0;
-    C3 fin = c3(0, 0, 0), bcol = c3(0, 0, 0), ret = def;
+    uint32_t n_prim = 0, n_shadow = 0, n_sec = 0;
     Frame stk[MAXD];
-    int sp = 0;
-    Closest c;
-    closest_init(c);
 
-    if (alive) {
-        // ray.rs:37-54 (aspect and fov_adjustment are per-frame constants)
-        double sx = ((((double)x + 0.5) / (double)a.width) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
-        double sy = (1.0 - (((double)y + 0.5) / (double)a.height) * 2.0) * a.fov_adjustment;
-        q.o = v3(0.0, 0.0, 0.0);
-        q.d = normalize(v3(sx, sy, -1.0));
-        n_prim = 1;
-        trace_primary(a, q.d, c);
-        mode = MODE_CLOSEST;
-        qdepth = 0;
-    }
-
-    bool have_result = alive;  // c / occl hold a fresh result for the lane's query
-    bool occl = false;
     for (;;) {
-        if (have_result) {
-            bool unwind = false;
-            bool shade = false;           // run a shade_diffuse step this iteration
-            const int rmode = mode;       // kind of result the lane holds
-            if (rmode == MODE_CLOSEST) {
-                if (c.nan && c.nhit >= 2) raise_error(a, pixel, RG_ERR_NAN_DISTANCE);
-                if (c.id < 0) {
-                    ret = def;  // rendering.rs:76-77, 128-129
-                    unwind = true;
-                } else {
-                    // get_color (rendering.rs:80-120)
-                    const RgBodyDev b = a.bodies[c.id];
-                    const RgMatDev m = a.mats[c.id];
-                    V3 h = add(q.o, scl(q.d, c.t));
-                    V3 n;
-                    if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
-                    if (m.surface != RG_SURFACE_REFRACTIVE) {
-                        float tx, ty;
-                        texture_coords(b, h, tx, ty);
-                        bcol = material_color(a, m, tx, ty);
-                        fin = c3(0.0f, 0.0f, 0.0f);
-                        hp = h; hn = n; hd = q.d; hb = c.id; hdepth = qdepth; li = 0;
-                        shade = true;
-                    } else {
-                        float kr = (float)fresnel(q.d, n, m.index);
-                        float tx, ty;
-                        texture_coords(b, h, tx, ty);
-                        C3 surf = material_color(a, m, tx, ty);
-                        Ray rr = reflection(n, q.d, h);
-                        int cd = qdepth + 1;
-                        C3 tc = def;
-                        bool trace_t = false;
-                        Ray tr;
-                        if (kr < 1.0f) {
-                            if (!transmission(n, q.d, h, m.index, tr)) raise_error(a, pixel, RG_ERR_TRANSMISSION);
-                            else if (cd < max_depth) trace_t = true;
-                        }
-                        if (cd >= max_depth) {
-                            C3 col = cadd(cscl(def, kr), cscl(tc, 1.0f - kr));
-                            ret = cmul(cscl(col, m.transparency), surf);
-                            unwind = true;
-                        } else {
-                            Frame &f = stk[sp++];
-                            f.f[0] = kr; f.f[1] = m.transparency;
-                            f.f[2] = surf.r; f.f[3] = surf.g; f.f[4] = surf.b;
-                            f.f[5] = tc.r; f.f[6] = tc.g; f.f[7] = tc.b;
-                            f.cdepth = cd;
-                            if (trace_t) {
-                                f.type = FR_REFR_T;
-                                f.rr[0] = rr.o.x; f.rr[1] = rr.o.y; f.rr[2] = rr.o.z;
-                                f.rr[3] = rr.d.x; f.rr[4] = rr.d.y; f.rr[5] = rr.d.z;
-                                q = tr;
-                            } else {
-                                f.type = FR_REFR_R;
-                                q = rr;
-                            }
-                            qdepth = cd;
-                            mode = MODE_CLOSEST;
-                            n_sec++;
-                        }
-                    }
-                }
-            } else {
-                shade = true;  // a shadow result for light li
-            }
-            if (shade) {
-                // shade_diffuse loop body (rendering.rs:141-170)
-                const RgMatDev m = a.mats[hb];
-                if (rmode == MODE_SHADOW) {
-                    const RgLightDev l = rg_cptr(a.lights)[li];
-                    float inten = !occl ? light_intensity(l, hp) : 0.0f;
-                    float power = fmaxf((float)dot(hn, q.d), 0.0f) * inten;
-                    float refl = m.albedo / PI_F;
-                    C3 lc = cscl(cscl(c3(l.color[0], l.color[1], l.color[2]), power), refl);
-                    fin = cadd(fin, cmul(bcol, lc));
-                    li++;
-                }
-                if (li < a.n_lights) {
-                    const RgLightDev l = rg_cptr(a.lights)[li];
-                    q.o = add(hp, scl(hn, SHADOW_BIAS));
-                    q.d = light_dir(l, hp);
-                    ld = light_distance(l, hp);
-                    mode = MODE_SHADOW;
-                    n_shadow++;
-                } else {
-                    C3 dcol = cclamp(fin);
-                    if (m.surface == RG_SURFACE_DIFFUSE) {
-                        ret = dcol;
+        uint32_t tile = 0;
+        if (lane == 0) tile = atomicAdd(reinterpret_cast<unsigned int *>(&a.counters[4]), 1u);
+        tile = __builtin_amdgcn_readfirstlane(__shfl(tile, 0, 64));
+        if (tile >= ntiles) break;
+        const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+        const uint32_t x = tx * 8u + (uint32_t)(lane & 7);
+        const uint32_t orow = ty * 8u + (uint32_t)(lane >> 3);
+        bool alive = x < a.width && orow < a.out_rows;
+        uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
+        const size_t oidx = (size_t)orow * a.width + x;
+        if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
+            a.rgba[oidx] = 0u;
+            if (a.rgb) { a.rgb[3 * oidx] = 0.0f; a.rgb[3 * oidx + 1] = 0.0f; a.rgb[3 * oidx + 2] = 0.0f; }
+            alive = false;
+        }
+        const uint32_t pixel = y * a.width + x;
+
+        int mode = MODE_DONE;
+        Ray q;                 // current query
+        double ld = 0.0;       // shadow: light distance
+        int qdepth = 0;        // closest: depth of the ray
+        // hit being shaded
+        V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0), hd = v3(0, 0, 0);
+        int hb = 0, hdepth = 0, li = 0;
+        C3 fin = c3(0, 0, 0), bcol = c3(0, 0, 0), ret = def;
+        int sp = 0;
+        Closest c;
+        closest_init(c);
+
+        if (alive) {
+            // ray.rs:37-54 (aspect and fov_adjustment are per-frame constants)
+            double sx = ((((double)x + 0.5) / (double)a.width) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
+            double sy = (1.0 - (((double)y + 0.5) / (double)a.height) * 2.0) * a.fov_adjustment;
+            q.o = v3(0.0, 0.0, 0.0);
+            q.d = normalize(v3(sx, sy, -1.0));
+            n_prim++;
+            trace_primary(a, src, q.d, c);
+            mode = MODE_CLOSEST;
+            qdepth = 0;
+        }
+
+        bool have_result = alive;  // c / occl hold a fresh result for the lane's query
+        bool occl = false;
+        for (;;) {
+            if (have_result) {
+                bool unwind = false;
+                bool shade = false;           // run a shade_diffuse step this iteration
+                const int rmode = mode;       // kind of result the lane holds
+                if (rmode == MODE_CLOSEST) {
+                    if (c.nan && c.nhit >= 2) raise_error(a, pixel, RG_ERR_NAN_DISTANCE);
+                    if (c.id < 0) {
+                        ret = def;  // rendering.rs:76-77, 128-129
                         unwind = true;
-                    } else {  // Reflecting (rendering.rs:86-91)
-                        float r = m.reflectivity;
-                        int cd = hdepth + 1;
-                        if (cd >= max_depth) {
-                            ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
-                            unwind = true;
+                    } else {
+                        // get_color (rendering.rs:80-120)
+                        const RgBodyDev b = a.bodies[c.id];
+                        const RgMatDev m = a.mats[c.id];
+                        V3 h = add(q.o, scl(q.d, c.t));
+                        V3 n;
+                        if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
+                        if (m.surface != RG_SURFACE_REFRACTIVE) {
+                            float tx, ty;
+                            texture_coords(b, h, tx, ty);
+                            bcol = material_color(a, m, tx, ty);
+                            fin = c3(0.0f, 0.0f, 0.0f);
+                            hp = h; hn = n; hd = q.d; hb = c.id; hdepth = qdepth; li = 0;
+                            shade = true;
                         } else {
-                            Frame &f = stk[sp++];
-                            f.type = FR_REFL;
-                            f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = r;
-                            f.cdepth = cd;
-                            q = reflection(hn, hd, hp);
-                            qdepth = cd;
+                            float kr = (float)fresnel(q.d, n, m.index);
+                            float tx, ty;
+                            texture_coords(b, h, tx, ty);
+                            C3 surf = material_color(a, m, tx, ty);
+                            Ray rr = reflection(n, q.d, h);
+                            int cd = qdepth + 1;
+                            C3 tc = def;
+                            bool trace_t = false;
+                            Ray tr;
+                            if (kr < 1.0f) {
+                                if (!transmission(n, q.d, h, m.index, tr)) raise_error(a, pixel, RG_ERR_TRANSMISSION);
+                                else if (cd < max_depth) trace_t = true;
+                            }
+                            if (cd >= max_depth) {
+                                C3 col = cadd(cscl(def, kr), cscl(tc, 1.0f - kr));
+                                ret = cmul(cscl(col, m.transparency), surf);
+                                unwind = true;
+                            } else {
+                                Frame &f = stk[sp++];
+                                f.f[0] = kr; f.f[1] = m.transparency;
+                                f.f[2] = surf.r; f.f[3] = surf.g; f.f[4] = surf.b;
+                                f.f[5] = tc.r; f.f[6] = tc.g; f.f[7] = tc.b;
+                                f.cdepth = cd;
+                                if (trace_t) {
+                                    f.type = FR_REFR_T;
+                                    f.rr[0] = rr.o.x; f.rr[1] = rr.o.y; f.rr[2] = rr.o.z;
+                                    f.rr[3] = rr.d.x; f.rr[4] = rr.d.y; f.rr[5] = rr.d.z;
+                                    q = tr;
+                                } else {
+                                    f.type = FR_REFR_R;
+                                    q = rr;
+                                }
+                                qdepth = cd;
+                                mode = MODE_CLOSEST;
+                                n_sec++;
+                            }
+                        }
+                    }
+                } else {
+                    shade = true;  // a shadow result for light li
+                }
+                if (shade) {
+                    // shade_diffuse loop body (rendering.rs:141-170)
+                    const RgMatDev m = a.mats[hb];
+                    if (rmode == MODE_SHADOW) {
+                        const RgLightDev l = rg_cptr(a.lights)[li];
+                        float inten = !occl ? light_intensity(l, hp) : 0.0f;
+                        float power = fmaxf((float)dot(hn, q.d), 0.0f) * inten;
+                        float refl = m.albedo / PI_F;
+                        C3 lc = cscl(cscl(c3(l.color[0], l.color[1], l.color[2]), power), refl);
+                        fin = cadd(fin, cmul(bcol, lc));
+                        li++;
+                    }
+                    if (li < a.n_lights) {
+                        const RgLightDev l = rg_cptr(a.lights)[li];
+                        q.o = add(hp, scl(hn, SHADOW_BIAS));
+                        q.d = light_dir(l, hp);
+                        ld = light_distance(l, hp);
+                        mode = MODE_SHADOW;
+                        n_shadow++;
+                    } else {
+                        C3 dcol = cclamp(fin);
+                        if (m.surface == RG_SURFACE_DIFFUSE) {
+                            ret = dcol;
+                            unwind = true;
+                        } else {  // Reflecting (rendering.rs:86-91)
+                            float r = m.reflectivity;
+                            int cd = hdepth + 1;
+                            if (cd >= max_depth) {
+                                ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
+                                unwind = true;
+                            } else {
+                                Frame &f = stk[sp++];
+                                f.type = FR_REFL;
+                                f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = r;
+                                f.cdepth = cd;
+                                q = reflection(hn, hd, hp);
+                                qdepth = cd;
+                                mode = MODE_CLOSEST;
+                                n_sec++;
+                            }
+                        }
+                    }
+                }
+                if (unwind) {
+                    for (;;) {
+                        if (sp == 0) {
+                            a.rgba[oidx] = f32_to_u8(ret.r * 255.0f) | (f32_to_u8(ret.g * 255.0f) << 8) |
+                                           (f32_to_u8(ret.b * 255.0f) << 16) | 0xFF000000u;
+                            if (a.rgb) { a.rgb[3 * oidx] = ret.r; a.rgb[3 * oidx + 1] = ret.g; a.rgb[3 * oidx + 2] = ret.b; }
+                            mode = MODE_DONE;
+                            break;
+                        }
+                        Frame &f = stk[sp - 1];
+                        if (f.type == FR_REFL) {
+                            ret = cadd(cscl(c3(f.f[0], f.f[1], f.f[2]), 1.0f - f.f[3]), cscl(ret, f.f[3]));
+                            sp--;
+                        } else if (f.type == FR_REFR_T) {
+                            f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
+                            f.type = FR_REFR_R;
+                            q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
+                            q.d = v3(f.rr[3], f.rr[4], f.rr[5]);
+                            qdepth = f.cdepth;
                             mode = MODE_CLOSEST;
                             n_sec++;
+                            break;
+                        } else {  // FR_REFR_R (rendering.rs:115-117)
+                            float kr = f.f[0];
+                            C3 col = cadd(cscl(ret, kr), cscl(c3(f.f[5], f.f[6], f.f[7]), 1.0f - kr));
+                            ret = cmul(cscl(col, f.f[1]), c3(f.f[2], f.f[3], f.f[4]));
+                            sp--;
                         }
                     }
                 }
             }
-            if (unwind) {
-                for (;;) {
-                    if (sp == 0) {
-                        a.rgba[oidx] = f32_to_u8(ret.r * 255.0f) | (f32_to_u8(ret.g * 255.0f) << 8) |
-                                       (f32_to_u8(ret.b * 255.0f) << 16) | 0xFF000000u;
-                        if (a.rgb) { a.rgb[3 * oidx] = ret.r; a.rgb[3 * oidx + 1] = ret.g; a.rgb[3 * oidx + 2] = ret.b; }
-                        mode = MODE_DONE;
-                        break;
-                    }
-                    Frame &f = stk[sp - 1];
-                    if (f.type == FR_REFL) {
-                        ret = cadd(cscl(c3(f.f[0], f.f[1], f.f[2]), 1.0f - f.f[3]), cscl(ret, f.f[3]));
-                        sp--;
-                    } else if (f.type == FR_REFR_T) {
-                        f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
-                        f.type = FR_REFR_R;
-                        q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
-                        q.d = v3(f.rr[3], f.rr[4], f.rr[5]);
-                        qdepth = f.cdepth;
-                        mode = MODE_CLOSEST;
-                        n_sec++;
-                        break;
-                    } else {  // FR_REFR_R (rendering.rs:115-117)
-                        float kr = f.f[0];
-                        C3 col = cadd(cscl(ret, kr), cscl(c3(f.f[5], f.f[6], f.f[7]), 1.0f - kr));
-                        ret = cmul(cscl(col, f.f[1]), c3(f.f[2], f.f[3], f.f[4]));
-                        sp--;
-                    }
-                }
+            const bool live = mode != MODE_DONE;
+            if (!__any(live)) break;
+            if (live) {
+                closest_init(c);
+                occl = false;
+                trace_query(a, src, q, mode == MODE_SHADOW, ld, c, occl);
             }
+            have_result = live;
         }
-        const bool live = mode != MODE_DONE;
-        if (!__any(live)) break;
-        if (live) {
-            closest_init(c);
-            occl = false;
-            trace_query(a, q, mode == MODE_SHADOW, ld, c, occl);
-        }
-        have_result = live;
+
     }
 
     // ray counters: wave reduction, one atomic per wave per class
-    n_prim = wave_sum(n_prim);
-    n_shadow = wave_sum(n_shadow);
-    n_sec = wave_sum(n_sec);
+    unsigned long long p64 = wave_sum(n_prim), s64 = wave_sum(n_shadow), q64 = wave_sum(n_sec);
     if (lane == 0) {
-        if (n_prim) atomicAdd(&a.counters[0], n_prim);
-        if (n_shadow) atomicAdd(&a.counters[1], n_shadow);
-        if (n_sec) atomicAdd(&a.counters[2], n_sec);
+        if (p64) atomicAdd(&a.counters[0], p64);
+        if (s64) atomicAdd(&a.counters[1], s64);
+        if (q64) atomicAdd(&a.counters[2], q64);
     }
 }
 
@@ -599,7 +692,8 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
     closest_init(c);
     bool occl = false;
     if (alive) {
-        trace_query(a, r, false, 0.0, c, occl);
+        SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc)};
+        trace_query(a, src, r, false, 0.0, c, occl);
         if (c.nan && c.nhit >= 2) raise_error(a, i, RG_ERR_NAN_DISTANCE);
         dist[i] = c.id >= 0 ? c.t : 0.0;
         body[i] = c.id;
@@ -607,14 +701,55 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
 }
 
 // ---------------------------------------------------------------- launchers
-extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {
-    dim3 grid((a->width + 15) / 16, (a->out_rows + 15) / 16);
-    dim3 block(256);
-    if (maxd <= 8) hipLaunchKernelGGL(rg_render_kernel<8>, grid, block, 0, stream, *a);
-    else if (maxd <= 16) hipLaunchKernelGGL(rg_render_kernel<16>, grid, block, 0, stream, *a);
-    else if (maxd <= 64) hipLaunchKernelGGL(rg_render_kernel<64>, grid, block, 0, stream, *a);
-    else return hipErrorInvalidValue;
+// Launch geometry: persistent 256-thread blocks, as many as fit on the device
+// (occupancy query x CUs), never more than the 8x8 tiles need.
+template <int MAXD, bool LDS, int MINW>
+static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream) {
+    static int cus = 0, per_cu_cache[2] = {0, 0};
+    static size_t lds_cache[2] = {~(size_t)0, ~(size_t)0};
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorInvalidValue;
+    }
+    int &per_cu = per_cu_cache[LDS ? 1 : 0];
+    if (lds_cache[LDS ? 1 : 0] != lds) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rg_render_kernel<MAXD, LDS, MINW>, 256, lds) != hipSuccess)
+            return hipErrorInvalidValue;
+        lds_cache[LDS ? 1 : 0] = lds;
+        if (per_cu < 1) per_cu = 1;
+    }
+    const unsigned long long tiles = (unsigned long long)((a->width + 7) / 8) * ((a->out_rows + 7) / 8);
+    unsigned long long blocks = (unsigned long long)cus * per_cu;
+    const unsigned long long need = (tiles + 3) / 4;
+    if (blocks > need) blocks = need;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL((rg_render_kernel<MAXD, LDS, MINW>), dim3((unsigned)blocks), dim3(256), lds, stream, *a);
     return hipGetLastError();
+}
+
+#ifndef RG_LDS_SPHERE_LIMIT
+#define RG_LDS_SPHERE_LIMIT (64 * 1024)  // bytes of sphere tables staged in LDS per block
+#endif
+
+#ifndef RG_HEAVY_SCENE_BODIES
+#define RG_HEAVY_SCENE_BODIES 32  // bodies per ray at which the trace loop, not shading, dominates
+#endif
+
+template <int MAXD>
+static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
+    const size_t lds = (size_t)a->n_sph * (sizeof(RgSph) + sizeof(double));
+    const bool use_lds = a->n_sph > 0 && lds <= RG_LDS_SPHERE_LIMIT;
+    const bool heavy = a->n_sph + a->n_pln + a->n_dsk + a->n_box >= RG_HEAVY_SCENE_BODIES;
+    if (heavy) return use_lds ? launch_one<MAXD, true, 4>(a, lds, stream) : launch_one<MAXD, false, 4>(a, 0, stream);
+    return use_lds ? launch_one<MAXD, true, 1>(a, lds, stream) : launch_one<MAXD, false, 1>(a, 0, stream);
+}
+
+extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {
+    if (maxd <= 8) return launch_depth<8>(a, stream);
+    if (maxd <= 16) return launch_depth<16>(a, stream);
+    if (maxd <= 64) return launch_depth<64>(a, stream);
+    return hipErrorInvalidValue;
 }
 
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,

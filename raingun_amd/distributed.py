@@ -1,0 +1,86 @@
+"""Row-tile sharding of one frame across ranks (one process per GPU).
+
+Pixels are independent (rendering.rs:27-33), so the frame is cut into
+`tile_rows`-row tiles dealt round-robin: tile t belongs to rank t % world
+(interleaving balances sky-heavy and geometry-heavy bands).  Each rank renders
+its tiles densely packed into one buffer of `slot_rows(...)` rows (the last
+ranks' buffers are zero-padded so every rank sends the same byte count), and
+ONE gather (torch.distributed; backend "nccl" is RCCL over xGMI) brings the
+buffers to rank 0, which re-interleaves them into image order.
+
+There is no other collective on the data path.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+TILE_ROWS = 16
+
+
+def n_tiles(height: int, tile_rows: int = TILE_ROWS) -> int:
+    return (height + tile_rows - 1) // tile_rows
+
+
+def tiles_per_rank(height: int, world: int, tile_rows: int = TILE_ROWS) -> int:
+    return (n_tiles(height, tile_rows) + world - 1) // world
+
+
+def slot_rows(height: int, world: int, tile_rows: int = TILE_ROWS) -> int:
+    """Rows of every rank's gather buffer (equal across ranks)."""
+    return tiles_per_rank(height, world, tile_rows) * tile_rows
+
+
+def rank_tiles(height: int, rank: int, world: int, tile_rows: int = TILE_ROWS) -> list:
+    return list(range(rank, n_tiles(height, tile_rows), world))
+
+
+def tiling(rank: int, world: int, tile_rows: int = TILE_ROWS):
+    """The rg_tiling a rank passes to rg_render_tiles[_async]."""
+    from ._abi import rg_tiling
+
+    return rg_tiling(tile_rows, world, rank)
+
+
+def assemble(gathered, height: int, world: int, tile_rows: int = TILE_ROWS):
+    """Re-interleave the per-rank buffers into image order.
+
+    `gathered` is a list (index = rank) of (slot_rows, W, C) tensors or arrays,
+    or one stacked (world, slot_rows, W, C) tensor/array.  Returns (height, W, C)."""
+    import numpy as np
+
+    is_np = isinstance(gathered, np.ndarray) or (isinstance(gathered, (list, tuple)) and
+                                                 isinstance(gathered[0], np.ndarray))
+    if is_np:
+        g = np.stack(gathered) if isinstance(gathered, (list, tuple)) else gathered
+    else:
+        import torch
+
+        g = torch.stack(list(gathered)) if isinstance(gathered, (list, tuple)) else gathered
+    tpr = tiles_per_rank(height, world, tile_rows)
+    w, c = g.shape[-2], g.shape[-1]
+    g = g.reshape(world, tpr, tile_rows, w, c)
+    # tile j*world + r lives in g[r, j]
+    g = g.transpose(1, 0, 2, 3, 4) if is_np else g.transpose(0, 1)
+    return g.reshape(world * tpr * tile_rows, w, c)[:height]
+
+
+def render_frame(render_tiles: Callable[[object], object], height: int, rank: int, world: int,
+                 tile_rows: int = TILE_ROWS, group=None, out=None, gather_bufs=None):
+    """Render this rank's tiles with `render_tiles(tiling) -> (slot_rows, W, 4)
+    tensor` and gather the frame to rank 0.  Returns the (height, W, 4) frame on
+    rank 0 and None on the other ranks."""
+    part = render_tiles(tiling(rank, world, tile_rows))
+    if world == 1:
+        return part[:height]
+    import torch.distributed as dist
+
+    if rank == 0:
+        bufs = gather_bufs if gather_bufs is not None else [part.new_empty(part.shape) for _ in range(world)]
+        dist.gather(part, bufs, dst=0, group=group)
+        frame = assemble(bufs, height, world, tile_rows)
+        if out is not None:
+            out.copy_(frame)
+            return out
+        return frame
+    dist.gather(part, None, dst=0, group=group)
+    return None

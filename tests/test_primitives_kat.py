@@ -1,0 +1,105 @@
+"""Known-answer tests of the restated primitives (oracle/raingun_oracle.c)
+derived from the reference formulas."""
+import math
+
+import numpy as np
+import pytest
+
+from raingun_amd.color import Color
+from raingun_amd.scene import AABB, Disk, Material, Plane, Scene, SceneDesc, Sphere
+
+
+def test_fresnel_bug_constant(oracle_lib):
+    """rendering.rs:194 sets cos_i = cos_t.abs(), collapsing kr to ((eta_t-eta_i)/(eta_t+eta_i))^2."""
+    idx = np.float32(1.33)
+    want = ((float(idx) - 1.0) / (float(idx) + 1.0)) ** 2
+    for inc in [(0.0, 0.0, -1.0), (0.3, 0.1, -0.9486832980505138), (0.6, 0.0, -0.8)]:
+        kr = oracle_lib.lib().rgo_fresnel(*inc, 0.0, 0.0, 1.0, idx)
+        assert kr == pytest.approx(want, rel=1e-12)
+    assert want == pytest.approx(0.020059, abs=1e-6)
+
+
+def test_fresnel_total_internal_reflection(oracle_lib):
+    # inside the body (i.n > 0) at a grazing angle: sin_t > 1 -> 1.0
+    kr = oracle_lib.lib().rgo_fresnel(0.9, 0.0, 0.4358898943540673, 0.0, 0.0, 1.0, np.float32(1.5))
+    assert kr == 1.0
+
+
+@pytest.mark.parametrize("val,size,want", [
+    (0.0, 512, 0), (0.5, 512, 256), (-0.25, 512, 384), (1.0, 512, 0), (-1.0, 512, 0),
+    (3.75, 100, 75), (-0.001, 1500, 1499), (float("nan"), 1500, 0),
+    (3.0e9, 1500, 2147483647 % 1500),            # saturating `as i32`
+    (-3.0e9, 1500, 1500 - (2147483648 % 1500)),  # i32::MIN % 1500 = -1148, +1500
+])
+def test_wrap(oracle_lib, val, size, want):  # material.rs:129-138
+    assert oracle_lib.lib().rgo_wrap(np.float32(val), size) == want
+
+
+@pytest.mark.parametrize("v,want", [(0.0, 0), (254.99, 254), (255.0, 255), (300.0, 255), (-3.0, 0),
+                                    (float("nan"), 0), (127.9999, 127)])
+def test_f32_to_u8(oracle_lib, v, want):
+    assert oracle_lib.lib().rgo_f32_to_u8(np.float32(v)) == want
+
+
+def test_fov_adjustment(oracle_lib):
+    assert oracle_lib.lib().rgo_fov_adjustment(90.0) == math.tan(90.0 * (math.pi / 180.0) / 2.0)
+
+
+M = Material(Color.from_str("#ffffff"), 0.5)
+
+
+def _trace(oracle_lib, bodies, o, d):
+    st, dist, body = oracle_lib.trace(SceneDesc(Scene(bodies=bodies)), np.array([*o, *d], float))
+    assert st == 0
+    return (None if body[0] < 0 else (float(dist[0]), int(body[0])))
+
+
+def test_sphere_hit_miss_inside(oracle_lib):
+    s = [Sphere((0.0, 0.0, -5.0), 1.0, M)]
+    assert _trace(oracle_lib, s, (0, 0, 0), (0, 0, -1)) == (4.0, 0)
+    assert _trace(oracle_lib, s, (0, 0, -5), (0, 0, -1)) == (1.0, 0)   # inside: far root
+    assert _trace(oracle_lib, s, (0, 0, 0), (0, 0, 1)) is None         # behind
+    assert _trace(oracle_lib, s, (0, 2, 0), (0, 0, -1)) is None        # miss
+
+
+def test_plane_is_one_sided(oracle_lib):
+    p = [Plane((0.0, -2.0, 0.0), (0.0, -1.0, 0.0), M)]
+    assert _trace(oracle_lib, p, (0, 0, 0), (0, -1, 0)) == (2.0, 0)
+    assert _trace(oracle_lib, p, (0, -3, 0), (0, 1, 0)) is None        # n.d <= 1e-6
+
+
+def test_disk_radius(oracle_lib):
+    d = [Disk((0.0, 0.0, -5.0), (0.0, 0.0, -1.0), 1.0, M)]
+    assert _trace(oracle_lib, d, (0, 0, 0), (0, 0, -1)) == (5.0, 0)
+    assert _trace(oracle_lib, d, (1.5, 0, 0), (0, 0, -1)) is None
+
+
+def test_aabb_inside_outside(oracle_lib):
+    b = [AABB(((-1.0, -1.0, -7.0), (1.0, 1.0, -5.0)), M)]
+    assert _trace(oracle_lib, b, (0, 0, 0), (0, 0, -1)) == (5.0, 0)
+    assert _trace(oracle_lib, b, (0, 0, -6), (0, 0, -1)) == (1.0, 0)   # inside: tmax
+    assert _trace(oracle_lib, b, (3, 0, 0), (0, 0, -1)) is None
+
+
+def test_first_minimum_tie_break(oracle_lib):
+    """Scene::trace keeps the FIRST of equal distances (min_by, scene.rs:34-39)."""
+    s = [Sphere((0.0, 0.0, -5.0), 1.0, M), Sphere((0.0, 0.0, -5.0), 1.0, M)]
+    assert _trace(oracle_lib, s, (0, 0, 0), (0, 0, -1)) == (4.0, 0)
+    p = [Plane((0.0, 0.0, -4.0), (0.0, 0.0, -1.0), M), Sphere((0.0, 0.0, -5.0), 1.0, M)]
+    assert _trace(oracle_lib, p, (0, 0, 0), (0, 0, -1)) == (4.0, 0)
+    p2 = [Sphere((0.0, 0.0, -5.0), 1.0, M), Plane((0.0, 0.0, -4.0), (0.0, 0.0, -1.0), M)]
+    assert _trace(oracle_lib, p2, (0, 0, 0), (0, 0, -1)) == (4.0, 0)
+
+
+def test_portrait_rejected(oracle_lib, example_scenes):
+    st, _, _, _, _ = oracle_lib.render(SceneDesc(example_scenes["test2"]), 60, 80)
+    assert st == -2  # RG_ERR_PORTRAIT (ray.rs:42)
+
+
+def test_depth_zero_still_shades_primary(oracle_lib, example_scenes):
+    """render_pixel traces and shades the primary ray even at max depth 0 (rendering.rs:71-78)."""
+    import copy
+    s = copy.copy(example_scenes["test2"])
+    s.max_recursion_depth = 0
+    _, rgba, _, counts, _ = oracle_lib.render(SceneDesc(s), 80, 60)
+    assert counts["primary"] == 4800 and counts["secondary"] == 0 and counts["shadow"] > 0
