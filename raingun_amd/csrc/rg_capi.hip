@@ -24,7 +24,7 @@ struct rg_scene {
     double fov = 90.0;
     float def[3] = {0, 0, 0};
     uint32_t max_depth = 10;
-    int32_t n_sph = 0, n_pln = 0, n_dsk = 0, n_box = 0, n_bodies = 0, n_lights = 0;
+    int32_t n_sph = 0, n_pln = 0, n_dsk = 0, n_box = 0, n_bodies = 0, n_lights = 0, n_textures = 0;
     std::vector<void *> allocations;
     RgSph *sph = nullptr;
     double *sph_cc = nullptr;
@@ -95,6 +95,16 @@ RgKernelArgs make_args(const rg_scene *s) {
     a.texs = s->texs;
     a.n_bodies = s->n_bodies;
     a.n_lights = s->n_lights;
+    a.n_textures = s->n_textures;
+    // LDS arena: [sph | cc (padded to 16 B) | bodies | mats | lights | texture descriptors]
+    auto al16 = [](uint32_t v) { return (v + 15u) & ~15u; };
+    a.lds_cc = (uint32_t)s->n_sph * (uint32_t)sizeof(RgSph);
+    a.lds_bodies = al16(a.lds_cc + (uint32_t)s->n_sph * 8u);
+    a.lds_hot_bytes = a.lds_bodies;
+    a.lds_mats = a.lds_bodies + (uint32_t)s->n_bodies * (uint32_t)sizeof(RgBodyDev);
+    a.lds_lights = al16(a.lds_mats + (uint32_t)s->n_bodies * (uint32_t)sizeof(RgMatDev));
+    a.lds_texs = a.lds_lights + (uint32_t)s->n_lights * (uint32_t)sizeof(RgLightDev);
+    a.lds_total_bytes = a.lds_texs + (uint32_t)s->n_textures * (uint32_t)sizeof(RgTexDev);
     a.def[0] = s->def[0];
     a.def[1] = s->def[1];
     a.def[2] = s->def[2];
@@ -207,7 +217,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
             // r2 = radius * radius and cc = (c.c) evaluated exactly as the per-ray
             // reference expressions (bodies.rs:95,97) -> bit-identical.
             sph.push_back(RgSph{p[0], p[1], p[2], p[3] * p[3]});
-            sph_cc.push_back(dot3(p, p));
+            sph_cc.push_back(dot3(p, p));  // padded to an even count after the loop
             sph_id.push_back((int32_t)i);
             break;
         case RG_BODY_PLANE:
@@ -224,6 +234,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
             break;
         }
     }
+    if (sph_cc.size() % 2) sph_cc.push_back(0.0);  // LDS staging copies 16-B units
     std::vector<RgLightDev> lights(d->n_lights);
     for (uint32_t i = 0; i < d->n_lights; ++i) {
         const rg_light &l = d->lights[i];
@@ -232,6 +243,14 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         lights[i].intensity = l.intensity;
         lights[i].pad = 0;
         std::memcpy(lights[i].v, l.v, sizeof lights[i].v);
+        // Directional: normalize(-direction) (lights.rs:48) is a per-light constant.
+        // Same IEEE ops in the same order as the device would run -> identical bits.
+        double nx = -l.v[0], ny = -l.v[1], nz = -l.v[2];
+        double inv = 1.0 / std::sqrt((nx * nx + ny * ny) + nz * nz);
+        lights[i].dn[0] = nx * inv;
+        lights[i].dn[1] = ny * inv;
+        lights[i].dn[2] = nz * inv;
+        lights[i].pad2 = 0.0;
     }
     s->n_sph = (int32_t)sph.size();
     s->n_pln = (int32_t)pln.size();
@@ -239,6 +258,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
     s->n_box = (int32_t)box.size();
     s->n_bodies = (int32_t)d->n_bodies;
     s->n_lights = (int32_t)d->n_lights;
+    s->n_textures = (int32_t)d->n_textures;
 
     rg_status st = RG_OK;
 #define RG_UP(dst, vec) \

@@ -56,7 +56,9 @@ struct RgLightDev {        // lights.rs:8-26
     float color[3];
     float intensity;
     int32_t pad;
-    double v[3];
+    double v[3];              // direction (Directional) or position (Spherical)
+    double dn[3];             // Directional: normalize(-direction) (lights.rs:48), a per-light constant
+    double pad2;              // 80 B: 16-B multiple for LDS staging
 };
 
 struct RgTexDev {
@@ -82,7 +84,9 @@ struct RgKernelArgs {
     const RgMatDev *mats;
     const RgLightDev *lights;
     const RgTexDev *texs;
-    int32_t n_bodies, n_lights;
+    int32_t n_bodies, n_lights, n_textures;
+    // LDS arena (byte offsets; used by the LDS-staged kernel variants)
+    uint32_t lds_cc, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
     // frame
     uint32_t width, height;
     uint32_t tile_rows, tile_stride, tile_offset, out_rows;

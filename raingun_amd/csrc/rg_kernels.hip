@@ -138,9 +138,8 @@ __device__ __forceinline__ bool disk_hit(const RgDsk &k, V3 o, V3 d, double &t) 
 
 // ---------------------------------------------------------------- sphere sources
 // The sphere tables are read with a wave-uniform index.  Two sources:
-//  * SphLds: the block stages the tables into LDS once (persistent blocks),
-//    then every test reads them with broadcast ds_read_b128 (always a hit,
-//    ~100-cycle latency hidden by prefetching the next record);
+//  * SphLds: the persistent block stages the tables into LDS once and every
+//    test reads them with broadcast ds_read_b128 (always a hit);
 //  * SphScalar: scalar loads through the constant address space (s_load,
 //    SGPR operands) for scenes whose tables exceed the LDS budget.
 struct SphScalar {
@@ -156,46 +155,73 @@ struct SphLds {
     __device__ __forceinline__ double getcc(int i) const { return cc[i]; }
 };
 
-// primary rays (origin 0): adj = c.d, opp = (c.c) - adj*adj  (8 FP64 ops)
-__device__ __forceinline__ void sph_primary_one(const RgKernelArgs &a, int i, const RgSph &s, double cc, V3 d,
-                                                Closest &c) {
-    double adj = (s.cx * d.x + s.cy * d.y) + s.cz * d.z;
-    double opp = cc - adj * adj;
-    if (!(opp > s.r2)) {
-        double t;
-        if (sphere_tail(s.r2, opp, adj, t)) closest_add(c, t, rg_cptr(a.sph_id)[i]);
+#ifndef RG_SPH_GROUP
+#define RG_SPH_GROUP 2   // spheres per miss-test group (one divergent branch per group)
+#endif
+
+// Primary rays start at the origin (ray.rs:53): h = c - 0 = c exactly, so
+// h.h = c.c is a per-sphere constant (bit-identical): 8 FP64 ops per sphere.
+template <int G, class Src>
+__device__ __forceinline__ void sph_primary_group(const RgKernelArgs &a, const Src &src, int i, V3 d, Closest &c) {
+    RgSph s[G];
+    double cc[G], adj[G], opp[G];
+    bool cand[G];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < G; ++k) { s[k] = src.get(i + k); cc[k] = src.getcc(i + k); }
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        adj[k] = (s[k].cx * d.x + s[k].cy * d.y) + s[k].cz * d.z;
+        opp[k] = cc[k] - adj[k] * adj[k];
+        cand[k] = !(opp[k] > s[k].r2);   // bodies.rs:99
+        any |= cand[k];
+    }
+    if (any) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            double t;
+            if (cand[k] && sphere_tail(s[k].r2, opp[k], adj[k], t)) closest_add(c, t, rg_cptr(a.sph_id)[i + k]);
+        }
     }
 }
 
 template <class Src>
 __device__ __forceinline__ void sph_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
-    const int n = a.n_sph;
-    if (n <= 0) return;
-    RgSph s = src.get(0);
-    double cc = src.getcc(0);
-    for (int i = 0; i < n; ++i) {
-        const int j = i + 1 < n ? i + 1 : i;  // prefetch the next record (clamped)
-        RgSph sn = src.get(j);
-        double ccn = src.getcc(j);
-        sph_primary_one(a, i, s, cc, d, c);
-        s = sn;
-        cc = ccn;
-    }
+    constexpr int G = RG_SPH_GROUP;
+    const int n = a.n_sph, nfull = n - n % G;
+    int i = 0;
+    for (; i < nfull; i += G) sph_primary_group<G>(a, src, i, d, c);
+    for (; i < n; ++i) sph_primary_group<1>(a, src, i, d, c);
 }
 
-// general rays: closest-hit (secondary) or any-hit (shadow, see trace_query)
-__device__ __forceinline__ void sph_query_one(const RgKernelArgs &a, int i, const RgSph &s, V3 o, V3 d, bool shadow,
-                                              double ld, Closest &c, bool &occl, bool &need) {
-    double hx = s.cx - o.x, hy = s.cy - o.y, hz = s.cz - o.z;
-    double adj = (hx * d.x + hy * d.y) + hz * d.z;
-    double opp = ((hx * hx + hy * hy) + hz * hz) - adj * adj;
-    if (!(opp > s.r2) && need) {
-        double t;
-        if (sphere_tail(s.r2, opp, adj, t)) {
-            if (shadow) {
-                if (!(t > ld)) { occl = true; need = false; }
-            } else {
-                closest_add(c, t, rg_cptr(a.sph_id)[i]);
+// General rays: closest-hit (secondary) or any-hit (shadow; see trace_query).
+template <int G, class Src>
+__device__ __forceinline__ void sph_query_group(const RgKernelArgs &a, const Src &src, int i, V3 o, V3 d,
+                                                bool shadow, double ld, Closest &c, bool &occl, bool &need) {
+    RgSph s[G];
+    double adj[G], opp[G];
+    bool cand[G];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < G; ++k) s[k] = src.get(i + k);
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        double hx = s[k].cx - o.x, hy = s[k].cy - o.y, hz = s[k].cz - o.z;     // bodies.rs:92
+        adj[k] = (hx * d.x + hy * d.y) + hz * d.z;                              // :93
+        opp[k] = ((hx * hx + hy * hy) + hz * hz) - adj[k] * adj[k];             // :95
+        cand[k] = !(opp[k] > s[k].r2);                                          // :97-101
+        any |= cand[k];
+    }
+    if (any && need) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            double t;
+            if (cand[k] && sphere_tail(s[k].r2, opp[k], adj[k], t)) {
+                if (shadow) {
+                    if (!(t > ld)) { occl = true; need = false; }
+                } else {
+                    closest_add(c, t, rg_cptr(a.sph_id)[i + k]);
+                }
             }
         }
     }
@@ -204,30 +230,25 @@ __device__ __forceinline__ void sph_query_one(const RgKernelArgs &a, int i, cons
 template <class Src>
 __device__ __forceinline__ bool sph_query(const RgKernelArgs &a, const Src &src, V3 o, V3 d, bool shadow, double ld,
                                           Closest &c, bool &occl, bool &need) {
-    const int n = a.n_sph;
-    if (n <= 0) return true;
-    RgSph s = src.get(0);
-    for (int i = 0; i < n; ++i) {
-        const int j = i + 1 < n ? i + 1 : i;
-        RgSph sn = src.get(j);
-        sph_query_one(a, i, s, o, d, shadow, ld, c, occl, need);
-        s = sn;
-        if ((i & 7) == 7 && !__any(need)) return false;
+    constexpr int G = RG_SPH_GROUP;
+    const int n = a.n_sph, nfull = n - n % G;
+    int i = 0;
+    for (; i < nfull; i += G) {
+        sph_query_group<G>(a, src, i, o, d, shadow, ld, c, occl, need);
+        if (((i / G) & 1) && !__any(need)) return false;
     }
+    for (; i < n; ++i) sph_query_group<1>(a, src, i, o, d, shadow, ld, c, occl, need);
     return __any(need);
 }
 
-// Primary rays start at the origin (ray.rs:53), so c - o == c exactly and the
-// sphere's h.h and the plane's v.n are per-body constants (bit-identical to
-// the reference's per-ray values).  8 FP64 ops per sphere instead of 16.
 template <class Src>
 __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
     sph_primary(a, src, d, c);
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = rg_cptr(a.pln)[i];
-        double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;
+        double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137
         if (den > 1e-6) {
-            double dist = p.on / den;
+            double dist = p.on / den;                           // v = o_p - 0 = o_p: v.n = o.n
             if (dist >= 0.0) closest_add(c, dist, rg_cptr(a.pln_id)[i]);
         }
     }
@@ -238,7 +259,7 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
         if (disk_hit(k, o, d, t)) closest_add(c, t, rg_cptr(a.dsk_id)[i]);
     }
     if (a.n_box > 0) {
-        V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+        V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);           // ray.rs:24
         int sx = inv.x < 0.0, sy = inv.y < 0.0, sz = inv.z < 0.0;
         for (int i = 0; i < a.n_box; ++i) {
             const RgBox b = rg_cptr(a.box)[i];
@@ -252,7 +273,7 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
 // A shadow ray is occluded iff some body has a hit distance t with
 // !(t > light_distance)  <=>  !(min t > light_distance)  (rendering.rs:152-155),
 // so a lane stops testing at its first such hit and the wave leaves the body
-// loop as soon as every lane that is still testing is a finished shadow ray.
+// loops as soon as every lane that is still testing is a finished shadow ray.
 template <class Src>
 __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &src, const Ray &r, bool shadow, double ld,
                                             Closest &c, bool &occl) {
@@ -261,7 +282,7 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
     if (!sph_query(a, src, o, d, shadow, ld, c, occl, need)) return;
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = rg_cptr(a.pln)[i];
-        double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;
+        double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137-148
         if (den > 1e-6 && need) {
             double vx = p.ox - o.x, vy = p.oy - o.y, vz = p.oz - o.z;
             double dist = ((vx * p.nx + vy * p.ny) + vz * p.nz) / den;
@@ -347,9 +368,9 @@ __device__ __forceinline__ uint32_t wrap(float v, int32_t max) {
 }
 
 // material.rs:115-148 + color.rs:26-30
-__device__ __forceinline__ C3 material_color(const RgKernelArgs &a, const RgMatDev &m, float tx, float ty) {
+__device__ __forceinline__ C3 material_color(const RgTexDev *texs, const RgMatDev &m, float tx, float ty) {
     if (m.coloration == RG_COLORATION_COLOR) return c3(m.color[0], m.color[1], m.color[2]);
-    const RgTexDev t = a.texs[m.tex];
+    const RgTexDev t = texs[m.tex];
     uint32_t x = wrap(tx + m.xoff, t.w);
     uint32_t y = wrap(ty + m.yoff, t.h);
     uint32_t px = t.texels[(size_t)y * (uint32_t)t.w + x];
@@ -397,7 +418,7 @@ __device__ __forceinline__ bool transmission(V3 n, V3 inc, V3 h, float index, Ra
 
 // lights.rs:46-58
 __device__ __forceinline__ V3 light_dir(const RgLightDev &l, V3 p) {
-    if (l.kind == RG_LIGHT_DIRECTIONAL) return normalize(neg(v3(l.v[0], l.v[1], l.v[2])));
+    if (l.kind == RG_LIGHT_DIRECTIONAL) return v3(l.dn[0], l.dn[1], l.dn[2]);  // normalize(-dir), precomputed
     return normalize(sub(v3(l.v[0], l.v[1], l.v[2]), p));
 }
 __device__ __forceinline__ double light_distance(const RgLightDev &l, V3 p) {
@@ -436,32 +457,57 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 
 using namespace rgk;
 
-// Persistent render kernel.  Each wave repeatedly takes the next 8x8 pixel
-// tile from an atomic queue (counters[4]) and runs the per-lane state machine
-// until all 64 lanes have written their pixel.  With LDS, the block first
-// stages the sphere tables (RgSph[n], then cc[n]) into dynamic LDS.
-// MINW = minimum waves per SIMD requested from the register allocator:
-// 1 lets shading-heavy scenes keep everything in registers (2 waves/SIMD),
-// 4 caps the kernel at 128 VGPRs (cold shading state spills to scratch) so
-// body-heavy scenes get twice the waves to hide LDS/FP64 latency.
-template <int MAXD, bool LDS, int MINW>
-__global__ __launch_bounds__(256, MINW) void rg_render_kernel(RgKernelArgs a) {
+// Per-launch view of the cold (shading) tables: LDS copies or global.
+struct Cold {
+    const RgBodyDev *bodies;
+    const RgMatDev *mats;
+    const RgLightDev *lights;
+    const RgTexDev *texs;
+};
+
+// Stage [src, src+bytes) into LDS at dst (both 16-B aligned, bytes % 16 == 0).
+__device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uint32_t bytes) {
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    const uint4 *g = reinterpret_cast<const uint4 *>(src);
+    for (uint32_t k = threadIdx.x; k < bytes / 16u; k += blockDim.x) d[k] = g[k];
+}
+
+// Persistent render kernel: ONE block of 256*WPS threads per CU (WPS waves
+// per SIMD).  The block stages the scene into LDS once (LSPH: sphere tables;
+// LCOLD: bodies, materials, lights, texture descriptors), then every wave
+// repeatedly takes the next 8x8 pixel tile from an atomic queue
+// (counters[4]) and runs the per-lane state machine until its 64 lanes have
+// written their pixels.
+template <int MAXD, bool LSPH, bool LCOLD, int WPS>
+__global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    typename std::conditional<LDS, SphLds, SphScalar>::type src;
-    if constexpr (LDS) {
-        const int n = a.n_sph;
-        uint4 *dst = reinterpret_cast<uint4 *>(smem);
-        const uint4 *gs = reinterpret_cast<const uint4 *>(a.sph);
-        for (int k = threadIdx.x; k < n * 2; k += blockDim.x) dst[k] = gs[k];
-        double *dcc = reinterpret_cast<double *>(smem + (size_t)n * sizeof(RgSph));
-        for (int k = threadIdx.x; k < n; k += blockDim.x) dcc[k] = a.sph_cc[k];
-        __syncthreads();
+    typename std::conditional<LSPH, SphLds, SphScalar>::type src;
+    Cold T;
+    if constexpr (LSPH) {
+        stage16(smem, a.sph, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSph));
+        stage16(smem + a.lds_cc, a.sph_cc, a.lds_bodies - a.lds_cc);
         src.s = reinterpret_cast<const RgSph *>(smem);
-        src.cc = dcc;
+        src.cc = reinterpret_cast<const double *>(smem + a.lds_cc);
     } else {
         src.s = rg_cptr(a.sph);
         src.cc = rg_cptr(a.sph_cc);
     }
+    if constexpr (LCOLD) {
+        stage16(smem + a.lds_bodies, a.bodies, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgBodyDev));
+        stage16(smem + a.lds_mats, a.mats, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgMatDev));
+        stage16(smem + a.lds_lights, a.lights, (uint32_t)a.n_lights * (uint32_t)sizeof(RgLightDev));
+        stage16(smem + a.lds_texs, a.texs, (uint32_t)a.n_textures * (uint32_t)sizeof(RgTexDev));
+        T.bodies = reinterpret_cast<const RgBodyDev *>(smem + a.lds_bodies);
+        T.mats = reinterpret_cast<const RgMatDev *>(smem + a.lds_mats);
+        T.lights = reinterpret_cast<const RgLightDev *>(smem + a.lds_lights);
+        T.texs = reinterpret_cast<const RgTexDev *>(smem + a.lds_texs);
+    } else {
+        T.bodies = a.bodies;
+        T.mats = a.mats;
+        T.lights = a.lights;
+        T.texs = a.texs;
+    }
+    if constexpr (LSPH || LCOLD) __syncthreads();
 
     const int lane = threadIdx.x & 63;
     const uint32_t tiles_x = (a.width + 7u) / 8u;
@@ -527,15 +573,15 @@ __global__ __launch_bounds__(256, MINW) void rg_render_kernel(RgKernelArgs a) {
                         unwind = true;
                     } else {
                         // get_color (rendering.rs:80-120)
-                        const RgBodyDev b = a.bodies[c.id];
-                        const RgMatDev m = a.mats[c.id];
+                        const RgBodyDev b = T.bodies[c.id];
+                        const RgMatDev m = T.mats[c.id];
                         V3 h = add(q.o, scl(q.d, c.t));
                         V3 n;
                         if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
                         if (m.surface != RG_SURFACE_REFRACTIVE) {
                             float tx, ty;
                             texture_coords(b, h, tx, ty);
-                            bcol = material_color(a, m, tx, ty);
+                            bcol = material_color(T.texs, m, tx, ty);
                             fin = c3(0.0f, 0.0f, 0.0f);
                             hp = h; hn = n; hd = q.d; hb = c.id; hdepth = qdepth; li = 0;
                             shade = true;
@@ -543,7 +589,7 @@ __global__ __launch_bounds__(256, MINW) void rg_render_kernel(RgKernelArgs a) {
                             float kr = (float)fresnel(q.d, n, m.index);
                             float tx, ty;
                             texture_coords(b, h, tx, ty);
-                            C3 surf = material_color(a, m, tx, ty);
+                            C3 surf = material_color(T.texs, m, tx, ty);
                             Ray rr = reflection(n, q.d, h);
                             int cd = qdepth + 1;
                             C3 tc = def;
@@ -583,7 +629,7 @@ __global__ __launch_bounds__(256, MINW) void rg_render_kernel(RgKernelArgs a) {
                 }
                 if (shade) {
                     // shade_diffuse loop body (rendering.rs:141-170)
-                    const RgMatDev m = a.mats[hb];
+                    const RgMatDev m = T.mats[hb];
                     if (rmode == MODE_SHADOW) {
                         const RgLightDev l = rg_cptr(a.lights)[li];
                         float inten = !occl ? light_intensity(l, hp) : 0.0f;
@@ -664,7 +710,6 @@ __global__ __launch_bounds__(256, MINW) void rg_render_kernel(RgKernelArgs a) {
             }
             have_result = live;
         }
-
     }
 
     // ray counters: wave reduction, one atomic per wave per class
@@ -701,48 +746,61 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
 }
 
 // ---------------------------------------------------------------- launchers
-// Launch geometry: persistent 256-thread blocks, as many as fit on the device
-// (occupancy query x CUs), never more than the 8x8 tiles need.
-template <int MAXD, bool LDS, int MINW>
+// One persistent block per CU slot: grid = CUs x (blocks per CU the register
+// and LDS budgets admit), capped by the tiles the frame has.
+template <int MAXD, bool LSPH, bool LCOLD, int WPS>
 static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream) {
-    static int cus = 0, per_cu_cache[2] = {0, 0};
-    static size_t lds_cache[2] = {~(size_t)0, ~(size_t)0};
+    static int cus = 0, per_cu = 0;
+    static size_t lds_cached = ~(size_t)0;
+    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS>;
     if (cus == 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorInvalidValue;
     }
-    int &per_cu = per_cu_cache[LDS ? 1 : 0];
-    if (lds_cache[LDS ? 1 : 0] != lds) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rg_render_kernel<MAXD, LDS, MINW>, 256, lds) != hipSuccess)
+    if (lds_cached != lds) {
+        if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return hipErrorInvalidValue;
-        lds_cache[LDS ? 1 : 0] = lds;
-        if (per_cu < 1) per_cu = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256 * WPS, lds) != hipSuccess)
+            return hipErrorInvalidValue;
+        if (per_cu < 1) return hipErrorInvalidConfiguration;
+        lds_cached = lds;
     }
     const unsigned long long tiles = (unsigned long long)((a->width + 7) / 8) * ((a->out_rows + 7) / 8);
+    const unsigned long long waves = (unsigned long long)WPS * 4;
     unsigned long long blocks = (unsigned long long)cus * per_cu;
-    const unsigned long long need = (tiles + 3) / 4;
+    const unsigned long long need = (tiles + waves - 1) / waves;
     if (blocks > need) blocks = need;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((rg_render_kernel<MAXD, LDS, MINW>), dim3((unsigned)blocks), dim3(256), lds, stream, *a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256 * WPS), lds, stream, *a);
     return hipGetLastError();
 }
 
-#ifndef RG_LDS_SPHERE_LIMIT
-#define RG_LDS_SPHERE_LIMIT (64 * 1024)  // bytes of sphere tables staged in LDS per block
+#ifndef RG_LDS_BUDGET
+#define RG_LDS_BUDGET (160 * 1024)       // one block per CU owns the CU's LDS
+#endif
+#ifndef RG_HEAVY_SCENE_BODIES
+#define RG_HEAVY_SCENE_BODIES 32         // bodies per ray at which the trace loop, not shading, dominates
 #endif
 
-#ifndef RG_HEAVY_SCENE_BODIES
-#define RG_HEAVY_SCENE_BODIES 32  // bodies per ray at which the trace loop, not shading, dominates
-#endif
+template <int MAXD, int WPS>
+static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream) {
+    if (a->lds_total_bytes <= RG_LDS_BUDGET)  // whole scene (empty sphere part if n_sph == 0)
+        return launch_one<MAXD, true, true, WPS>(a, a->lds_total_bytes, stream);
+    if (a->n_sph > 0 && a->lds_hot_bytes <= RG_LDS_BUDGET)
+        return launch_one<MAXD, true, false, WPS>(a, a->lds_hot_bytes, stream);
+    return launch_one<MAXD, false, false, WPS>(a, 0, stream);
+}
 
 template <int MAXD>
 static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
-    const size_t lds = (size_t)a->n_sph * (sizeof(RgSph) + sizeof(double));
-    const bool use_lds = a->n_sph > 0 && lds <= RG_LDS_SPHERE_LIMIT;
+#if defined(RG_FORCE_WPS)
+    return launch_waves<MAXD, RG_FORCE_WPS>(a, stream);
+#else
     const bool heavy = a->n_sph + a->n_pln + a->n_dsk + a->n_box >= RG_HEAVY_SCENE_BODIES;
-    if (heavy) return use_lds ? launch_one<MAXD, true, 4>(a, lds, stream) : launch_one<MAXD, false, 4>(a, 0, stream);
-    return use_lds ? launch_one<MAXD, true, 1>(a, lds, stream) : launch_one<MAXD, false, 1>(a, 0, stream);
+    return heavy ? launch_waves<MAXD, 4>(a, stream) : launch_waves<MAXD, 2>(a, stream);
+#endif
 }
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {
