@@ -36,7 +36,7 @@ struct rg_scene {
     RgMatDev *mats = nullptr;
     RgLightDev *lights = nullptr;
     RgTexDev *texs = nullptr;
-    unsigned long long *counters = nullptr;  // 8 words (rg_device.h)
+    unsigned long long *counters = nullptr;  // RG_COUNTER_WORDS words (rg_device.h)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -292,7 +292,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
     if (st == RG_OK) st = upload(s, &s->texs, texs.data(), texs.size());
     if (st == RG_OK) {
         void *p = nullptr;
-        if (!ok(hipMalloc(&p, 8 * sizeof(unsigned long long)))) st = RG_ERR_OUT_OF_MEMORY;
+        if (!ok(hipMalloc(&p, RG_COUNTER_WORDS * sizeof(unsigned long long)))) st = RG_ERR_OUT_OF_MEMORY;
         else { s->allocations.push_back(p); s->counters = static_cast<unsigned long long *>(p); }
     }
     if (st == RG_OK && (!ok(hipEventCreate(&s->ev0)) || !ok(hipEventCreate(&s->ev1)))) st = RG_ERR_DEVICE;
@@ -329,7 +329,7 @@ rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t heig
     a.aspect = (double)width / (double)height;
     a.rgba = reinterpret_cast<uint32_t *>(rgba_dev);
     a.rgb = rgb_dev;
-    if (!ok(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
+    if (!ok(hipMemsetAsync(s->counters, 0, RG_COUNTER_WORDS * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
     if (out_rows == 0) return RG_OK;
     if (stats && !ok(hipEventRecord(s->ev0, st))) return RG_ERR_DEVICE;
     if (!ok(rg_launch_render(&a, frames_needed(s->max_depth), st))) return RG_ERR_DEVICE;

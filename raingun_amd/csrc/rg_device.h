@@ -97,8 +97,10 @@ struct RgKernelArgs {
     // outputs
     uint32_t *rgba;          // packed RGBA8, out_rows * width
     float *rgb;              // nullable, out_rows * width * 3
-    unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=~error key [4]=tile queue
+    unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=~error key [16+16q]=tile queue heads (RG_COUNTER_WORDS words)
 };
+
+#define RG_COUNTER_WORDS (16 + 16 * 16)  // stats + 16 queue heads, 128 B apart
 
 // counters[3] holds ~((pixel << 8) | -status) of the lowest erroring pixel
 // (atomicMax of the complement); 0 = no error, so one memset resets all four.

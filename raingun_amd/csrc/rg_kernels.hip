@@ -345,6 +345,9 @@ __device__ __forceinline__ bool surface_normal(const RgBodyDev &b, V3 h, V3 &n) 
 __device__ __forceinline__ void texture_coords(const RgBodyDev &b, V3 h, float &tx, float &ty) {
     if (b.kind == RG_BODY_SPHERE) {
         V3 hv = sub(h, bp3(b, 0));
+#ifdef RG_DBG_NO_ATAN  // timing ablation only (wrong images)
+        tx = (float)hv.x; ty = (float)hv.y; return;
+#endif
         tx = (1.0f + ((float)atan2(hv.z, hv.x)) / PI_F) * 0.5f;
         ty = ((float)acos(hv.y / b.p[3])) / PI_F;
     } else if (b.kind == RG_BODY_AABB) {
@@ -370,6 +373,9 @@ __device__ __forceinline__ uint32_t wrap(float v, int32_t max) {
 // material.rs:115-148 + color.rs:26-30
 __device__ __forceinline__ C3 material_color(const RgTexDev *texs, const RgMatDev &m, float tx, float ty) {
     if (m.coloration == RG_COLORATION_COLOR) return c3(m.color[0], m.color[1], m.color[2]);
+#ifdef RG_DBG_NO_TEX  // timing ablation only (wrong images)
+    return c3(0.5f, 0.5f, 0.5f);
+#endif
     const RgTexDev t = texs[m.tex];
     uint32_t x = wrap(tx + m.xoff, t.w);
     uint32_t y = wrap(ty + m.yoff, t.h);
@@ -457,6 +463,18 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 
 using namespace rgk;
 
+#ifndef RG_NQ
+#define RG_NQ 8   // tile-queue heads (see the kernel's tile loop)
+#endif
+#ifndef RG_Q_HOME_BY_BLOCK
+#define RG_Q_HOME_BY_BLOCK 1
+#endif
+#ifndef RG_Q_INTERLEAVE
+#define RG_Q_INTERLEAVE 1
+#endif
+#define RG_QUEUE_BASE 16   // counters[16 + 16*q]: head q, one 128-B line each
+#define RG_QUEUE_STRIDE 16
+
 // Per-launch view of the cold (shading) tables: LDS copies or global.
 struct Cold {
     const RgBodyDev *bodies;
@@ -476,7 +494,7 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // per SIMD).  The block stages the scene into LDS once (LSPH: sphere tables;
 // LCOLD: bodies, materials, lights, texture descriptors), then every wave
 // repeatedly takes the next 8x8 pixel tile from an atomic queue
-// (counters[4]) and runs the per-lane state machine until its 64 lanes have
+// (counters[16..], sharded) and runs the per-lane state machine until its 64 lanes have
 // written their pixels.
 template <int MAXD, bool LSPH, bool LCOLD, int WPS>
 __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
@@ -517,11 +535,38 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     uint32_t n_prim = 0, n_shadow = 0, n_sec = 0;
     Frame stk[MAXD];
 
+    // Sharded tile queue: RG_NQ heads, each owning a contiguous band of tiles
+    // (one 128-B line per head).  A single head saturates at ~88 dequeues/us
+    // (MI355X_MICROARCH.md "dequeue"), i.e. ~1.5 ms for a 4K frame of 8x8
+    // tiles; a wave starts on head (global wave id % RG_NQ) and moves to the
+    // next head when its band is exhausted (work stealing for the tail).
+    const uint32_t gwave = blockIdx.x * (blockDim.x / 64u) + (threadIdx.x >> 6);
+#if RG_Q_HOME_BY_BLOCK
+    uint32_t qi = blockIdx.x % RG_NQ, qtried = 0;  // a CU's waves share a head: adjacent tiles per CU
+    (void)gwave;
+#else
+    uint32_t qi = gwave % RG_NQ, qtried = 0;
+#endif
     for (;;) {
-        uint32_t tile = 0;
-        if (lane == 0) tile = atomicAdd(reinterpret_cast<unsigned int *>(&a.counters[4]), 1u);
-        tile = __builtin_amdgcn_readfirstlane(__shfl(tile, 0, 64));
-        if (tile >= ntiles) break;
+        uint32_t tile = 0xFFFFFFFFu;
+        while (qtried < RG_NQ) {
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(reinterpret_cast<unsigned int *>(&a.counters[RG_QUEUE_BASE + RG_QUEUE_STRIDE * qi]), 1u);
+            k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
+#if RG_Q_INTERLEAVE
+            // head q serves tiles q, q+NQ, q+2NQ, ...: the tiles in flight stay a
+            // compact raster-order band of the frame, as with a single head
+            const unsigned long long t = (unsigned long long)k * RG_NQ + qi;
+            if (t < ntiles) { tile = (uint32_t)t; break; }
+#else
+            const uint32_t lo = (uint32_t)(((unsigned long long)ntiles * qi) / RG_NQ);
+            const uint32_t hi = (uint32_t)(((unsigned long long)ntiles * (qi + 1)) / RG_NQ);
+            if (lo + k < hi) { tile = lo + k; break; }
+#endif
+            qi = (qi + 1) % RG_NQ;
+            ++qtried;
+        }
+        if (tile == 0xFFFFFFFFu) break;
         const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
         const uint32_t x = tx * 8u + (uint32_t)(lane & 7);
         const uint32_t orow = ty * 8u + (uint32_t)(lane >> 3);
@@ -706,6 +751,11 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             if (live) {
                 closest_init(c);
                 occl = false;
+#if defined(RG_DBG_NO_SHADOW_TRACE)  // timing ablation only (wrong images)
+                if (mode != MODE_SHADOW)
+#elif defined(RG_DBG_NO_SEC_TRACE)
+                if (mode == MODE_SHADOW)
+#endif
                 trace_query(a, src, q, mode == MODE_SHADOW, ld, c, occl);
             }
             have_result = live;
