@@ -324,6 +324,110 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
     }
 }
 
+// ---------------------------------------------------------------- shadow batches
+// shade_diffuse traces one shadow ray per light from the SAME origin
+// hit + n*bias (rendering.rs:141-150).  A lane traces up to RG_LB of them in
+// one pass: per sphere the origin-dependent part (h = c - o, h.h) is computed
+// once and only adj/opp/compare are per light, so a 3-light batch costs
+// 8 + 3*8 FP64 ops per sphere instead of 3*16, with bit-identical per-ray
+// arithmetic.  Bit l of `occl` = light l of the batch is occluded.
+#ifndef RG_LB
+#define RG_LB 3            // lights per shadow batch for light scenes (LB template parameter)
+#endif
+#ifndef RG_SHADOW_GROUP
+#define RG_SHADOW_GROUP 2  // spheres per miss-test group in the shadow pass
+#endif
+
+template <int LB>
+struct ShadowBatch {
+    V3 d[LB];           // direction_from(light) (lights.rs:46-51)
+    double ld[LB];      // light.distance(hit) (lights.rs:53-58), +inf for directional
+};
+
+template <int LB, class Src>
+__device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &src, V3 o, const ShadowBatch<LB> &sb,
+                                             uint32_t full, uint32_t &occl) {
+    constexpr int G = RG_SHADOW_GROUP;
+    const int n = a.n_sph, nfull = n - n % G;
+    for (int i = 0; i < n;) {
+        const int g = i < nfull ? G : 1;  // wave-uniform
+        RgSph s[G];
+        double hx[G], hy[G], hz[G], hh[G], adj[G][LB], opp[G][LB];
+        bool cand[G][LB];
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            if (k < g) {
+                s[k] = src.get(i + k);
+                hx[k] = s[k].cx - o.x; hy[k] = s[k].cy - o.y; hz[k] = s[k].cz - o.z;   // bodies.rs:92
+                hh[k] = (hx[k] * hx[k] + hy[k] * hy[k]) + hz[k] * hz[k];                // :95 (first term)
+#pragma unroll
+                for (int l = 0; l < LB; ++l) {
+                    adj[k][l] = (hx[k] * sb.d[l].x + hy[k] * sb.d[l].y) + hz[k] * sb.d[l].z;   // :93
+                    opp[k][l] = hh[k] - adj[k][l] * adj[k][l];                               // :95
+                    cand[k][l] = !(opp[k][l] > s[k].r2) && !((occl >> l) & 1u);              // :99
+                    any |= cand[k][l];
+                }
+            }
+        }
+        if (any) {
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+#pragma unroll
+                for (int l = 0; l < LB; ++l) {
+                    double t;
+                    if (k < g && cand[k][l] && sphere_tail(s[k].r2, opp[k][l], adj[k][l], t) && !(t > sb.ld[l]))
+                        occl |= 1u << l;
+                }
+            }
+        }
+        i += g;
+        if ((i & 7) == 0 && !__any(occl != full)) return;
+    }
+    if (!__any(occl != full)) return;
+    for (int i = 0; i < a.n_pln; ++i) {
+        const RgPln p = rg_cptr(a.pln)[i];
+        const double vx = p.ox - o.x, vy = p.oy - o.y, vz = p.oz - o.z;     // bodies.rs:139
+        const double num = (vx * p.nx + vy * p.ny) + vz * p.nz;             // :140 numerator
+#pragma unroll
+        for (int l = 0; l < LB; ++l) {
+            const double den = (p.nx * sb.d[l].x + p.ny * sb.d[l].y) + p.nz * sb.d[l].z;  // :137
+            if (den > 1e-6 && !((occl >> l) & 1u)) {
+                bool hit;
+                if (sb.ld[l] == __builtin_inf() && num >= 0.0) {
+                    hit = true;  // fl(num/den) >= 0 and !(fl(num/den) > inf): no division needed
+                } else {
+                    const double dist = num / den;
+                    hit = dist >= 0.0 && !(dist > sb.ld[l]);
+                }
+                if (hit) occl |= 1u << l;
+            }
+        }
+    }
+    if (!__any(occl != full)) return;
+    for (int i = 0; i < a.n_dsk; ++i) {
+        const RgDsk k = rg_cptr(a.dsk)[i];
+#pragma unroll
+        for (int l = 0; l < LB; ++l) {
+            double t;
+            if (!((occl >> l) & 1u) && disk_hit(k, o, sb.d[l], t) && !(t > sb.ld[l])) occl |= 1u << l;
+        }
+    }
+    if (a.n_box > 0 && __any(occl != full)) {
+#pragma unroll
+        for (int l = 0; l < LB; ++l) {
+            const V3 d = sb.d[l];
+            const V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+            const int sx = inv.x < 0.0, sy = inv.y < 0.0, sz = inv.z < 0.0;
+            for (int i = 0; i < a.n_box; ++i) {
+                const RgBox b = rg_cptr(a.box)[i];
+                double t;
+                if (!((occl >> l) & 1u) && aabb_hit(b, o, inv, sx, sy, sz, t) && !(t > sb.ld[l])) occl |= 1u << l;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- shading
 __device__ __forceinline__ V3 bp3(const RgBodyDev &b, int k) { return v3(b.p[k], b.p[k + 1], b.p[k + 2]); }
 
@@ -422,6 +526,20 @@ __device__ __forceinline__ bool transmission(V3 n, V3 inc, V3 h, float index, Ra
     return true;
 }
 
+// direction_from + distance for one light (lights.rs:46-58).  For a spherical
+// light both use |pos - p| = sqrt(dot(v, v)): computed once, same bits.
+__device__ __forceinline__ void light_dir_dist(const RgLightDev &l, V3 p, V3 &dir, double &dist) {
+    if (l.kind == RG_LIGHT_DIRECTIONAL) {
+        dir = v3(l.dn[0], l.dn[1], l.dn[2]);  // normalize(-direction), precomputed
+        dist = __builtin_inf();
+        return;
+    }
+    V3 v = sub(v3(l.v[0], l.v[1], l.v[2]), p);
+    double m = sqrt(dot(v, v));
+    dir = scl(v, 1.0 / m);
+    dist = m;
+}
+
 // lights.rs:46-58
 __device__ __forceinline__ V3 light_dir(const RgLightDev &l, V3 p) {
     if (l.kind == RG_LIGHT_DIRECTIONAL) return v3(l.dn[0], l.dn[1], l.dn[2]);  // normalize(-dir), precomputed
@@ -496,7 +614,7 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // repeatedly takes the next 8x8 pixel tile from an atomic queue
 // (counters[16..], sharded) and runs the per-lane state machine until its 64 lanes have
 // written their pixels.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS>
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB>
 __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     typename std::conditional<LSPH, SphLds, SphScalar>::type src;
@@ -581,8 +699,9 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         const uint32_t pixel = y * a.width + x;
 
         int mode = MODE_DONE;
-        Ray q;                 // current query
-        double ld = 0.0;       // shadow: light distance
+        Ray q;                 // current query (shadow: q.o = shared origin)
+        ShadowBatch<LB> sb;        // shadow: the batch's directions and light distances
+        uint32_t occl_full = 0u;
         int qdepth = 0;        // closest: depth of the ray
         // hit being shaded
         V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0), hd = v3(0, 0, 0);
@@ -605,7 +724,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         }
 
         bool have_result = alive;  // c / occl hold a fresh result for the lane's query
-        bool occl = false;
+        uint32_t occl = 0u;
         for (;;) {
             if (have_result) {
                 bool unwind = false;
@@ -673,24 +792,37 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                     shade = true;  // a shadow result for light li
                 }
                 if (shade) {
-                    // shade_diffuse loop body (rendering.rs:141-170)
+                    // shade_diffuse loop body (rendering.rs:141-170), LB lights per batch
                     const RgMatDev m = T.mats[hb];
                     if (rmode == MODE_SHADOW) {
-                        const RgLightDev l = rg_cptr(a.lights)[li];
-                        float inten = !occl ? light_intensity(l, hp) : 0.0f;
-                        float power = fmaxf((float)dot(hn, q.d), 0.0f) * inten;
-                        float refl = m.albedo / PI_F;
-                        C3 lc = cscl(cscl(c3(l.color[0], l.color[1], l.color[2]), power), refl);
-                        fin = cadd(fin, cmul(bcol, lc));
-                        li++;
+                        const float refl = m.albedo / PI_F;
+#pragma unroll
+                        for (int l = 0; l < LB; ++l) {
+                            if (li + l < a.n_lights) {
+                                const RgLightDev L = T.lights[li + l];
+                                float inten = !((occl >> l) & 1u) ? light_intensity(L, hp) : 0.0f;
+                                float power = fmaxf((float)dot(hn, sb.d[l]), 0.0f) * inten;
+                                C3 lc = cscl(cscl(c3(L.color[0], L.color[1], L.color[2]), power), refl);
+                                fin = cadd(fin, cmul(bcol, lc));
+                            }
+                        }
+                        li += LB;
                     }
                     if (li < a.n_lights) {
-                        const RgLightDev l = rg_cptr(a.lights)[li];
-                        q.o = add(hp, scl(hn, SHADOW_BIAS));
-                        q.d = light_dir(l, hp);
-                        ld = light_distance(l, hp);
+                        q.o = add(hp, scl(hn, SHADOW_BIAS));  // rendering.rs:148
+                        occl_full = 0u;
+#pragma unroll
+                        for (int l = 0; l < LB; ++l) {
+                            if (li + l < a.n_lights) {
+                                light_dir_dist(T.lights[li + l], hp, sb.d[l], sb.ld[l]);
+                                occl_full |= 1u << l;
+                                n_shadow++;
+                            } else {
+                                sb.d[l] = v3(0.0, 0.0, 1.0);
+                                sb.ld[l] = 0.0;
+                            }
+                        }
                         mode = MODE_SHADOW;
-                        n_shadow++;
                     } else {
                         C3 dcol = cclamp(fin);
                         if (m.surface == RG_SURFACE_DIFFUSE) {
@@ -750,13 +882,34 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             if (!__any(live)) break;
             if (live) {
                 closest_init(c);
-                occl = false;
-#if defined(RG_DBG_NO_SHADOW_TRACE)  // timing ablation only (wrong images)
-                if (mode != MODE_SHADOW)
-#elif defined(RG_DBG_NO_SEC_TRACE)
-                if (mode == MODE_SHADOW)
+                occl = 0u;
+            }
+            if constexpr (LB == 1) {
+                // one ray per lane, one pass: closest-hit and shadow lanes share the
+                // body loop (best when a wave mixes ray kinds over many bodies)
+                if (live) {
+                    bool o1 = false;
+                    Ray r1;
+                    r1.o = q.o;
+                    r1.d = mode == MODE_SHADOW ? sb.d[0] : q.d;
+                    trace_query(a, src, r1, mode == MODE_SHADOW, sb.ld[0], c, o1);
+                    occl = o1 ? 1u : 0u;
+                }
+            } else {
+                // closest-hit lanes and shadow-batch lanes walk the body tables in two
+                // passes; each pass is skipped when no lane of the wave needs it
+                if (mode == MODE_CLOSEST) {
+#ifndef RG_DBG_NO_SEC_TRACE
+                    bool unused = false;
+                    trace_query(a, src, q, false, 0.0, c, unused);
 #endif
-                trace_query(a, src, q, mode == MODE_SHADOW, ld, c, occl);
+                }
+                if (mode == MODE_SHADOW) {
+                    occl = ~occl_full & ((1u << LB) - 1u);  // absent slots count as done
+#ifndef RG_DBG_NO_SHADOW_TRACE
+                    trace_shadow<LB>(a, src, q.o, sb, (1u << LB) - 1u, occl);
+#endif
+                }
             }
             have_result = live;
         }
@@ -798,11 +951,11 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
 // ---------------------------------------------------------------- launchers
 // One persistent block per CU slot: grid = CUs x (blocks per CU the register
 // and LDS budgets admit), capped by the tiles the frame has.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS>
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB>
 static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream) {
     static int cus = 0, per_cu = 0;
     static size_t lds_cached = ~(size_t)0;
-    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS>;
+    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB>;
     if (cus == 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
@@ -834,23 +987,27 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
 #define RG_HEAVY_SCENE_BODIES 32         // bodies per ray at which the trace loop, not shading, dominates
 #endif
 
-template <int MAXD, int WPS>
+template <int MAXD, int WPS, int LB>
 static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream) {
     if (a->lds_total_bytes <= RG_LDS_BUDGET)  // whole scene (empty sphere part if n_sph == 0)
-        return launch_one<MAXD, true, true, WPS>(a, a->lds_total_bytes, stream);
+        return launch_one<MAXD, true, true, WPS, LB>(a, a->lds_total_bytes, stream);
     if (a->n_sph > 0 && a->lds_hot_bytes <= RG_LDS_BUDGET)
-        return launch_one<MAXD, true, false, WPS>(a, a->lds_hot_bytes, stream);
-    return launch_one<MAXD, false, false, WPS>(a, 0, stream);
+        return launch_one<MAXD, true, false, WPS, LB>(a, a->lds_hot_bytes, stream);
+    return launch_one<MAXD, false, false, WPS, LB>(a, 0, stream);
 }
 
 template <int MAXD>
 static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
+    // Light scenes (few bodies): per-iteration overhead dominates -> fewer,
+    // fatter iterations (RG_LB shadow rays per pass) at 2 waves/SIMD.  Heavy
+    // scenes: the body loop dominates and waves mix ray kinds -> one ray per
+    // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
 #if defined(RG_FORCE_WPS)
-    return launch_waves<MAXD, RG_FORCE_WPS>(a, stream);
+    const bool heavy = RG_FORCE_WPS == 4;
 #else
     const bool heavy = a->n_sph + a->n_pln + a->n_dsk + a->n_box >= RG_HEAVY_SCENE_BODIES;
-    return heavy ? launch_waves<MAXD, 4>(a, stream) : launch_waves<MAXD, 2>(a, stream);
 #endif
+    return heavy ? launch_waves<MAXD, 4, 1>(a, stream) : launch_waves<MAXD, 2, RG_LB>(a, stream);
 }
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {
