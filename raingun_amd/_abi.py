@@ -124,6 +124,9 @@ EXPORTED_SYMBOLS = (
     "rg_render_stream",
     "rg_trace",
 )
+# include/raingun_debug.h
+DEBUG_SYMBOLS = ("rg_debug_set_path",)
+PATH_AUTO, PATH_LIGHT, PATH_HEAVY = -1, 0, 1
 
 
 class RaingunError(RuntimeError):
@@ -163,6 +166,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_render_stream.restype = C.c_int32
     lib.rg_render_stream.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, TILE_CALLBACK, C.c_void_p,
                                      P(rg_stats)]
+    lib.rg_debug_set_path.restype = C.c_int32
+    lib.rg_debug_set_path.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_trace.restype = C.c_int32
     lib.rg_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
 

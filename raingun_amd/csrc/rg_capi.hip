@@ -4,6 +4,7 @@
 // batch closest-hit query.  No exception or abort crosses the ABI.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -11,6 +12,7 @@
 #include <vector>
 
 #include "../../include/raingun.h"
+#include "../../include/raingun_debug.h"
 #include "rg_device.h"
 
 #pragma clang fp contract(off)
@@ -28,6 +30,9 @@ struct rg_scene {
     std::vector<void *> allocations;
     RgSph *sph = nullptr;
     double *sph_cc = nullptr;
+    RgSphF *sphf = nullptr;
+    RgSphF2 *sphf2 = nullptr;
+    int32_t path = RG_PATH_AUTO;
     int32_t *sph_id = nullptr, *pln_id = nullptr, *dsk_id = nullptr, *box_id = nullptr;
     RgPln *pln = nullptr;
     RgDsk *dsk = nullptr;
@@ -60,6 +65,29 @@ rg_status upload(rg_scene *s, T **dst, const T *src, size_t n) {
 
 double dot3(const double *a, const double *b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
 
+// smallest float >= v (v finite, >= 0)
+float f32_up(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, HUGE_VALF);
+    return f;
+}
+
+// f32 pre-filter records of one sphere (bound derivation: rg_kernels.hip, "f32 pre-filter").
+void make_filter_records(const double *p, RgSphF &f, RgSphF2 &f2) {
+    const double u = 5.9604644775390625e-08;  // 2^-24
+    const double r2 = p[3] * p[3];            // the reference's radius * radius (bodies.rs:97)
+    const double cc = dot3(p, p);
+    f.cx = (float)p[0];
+    f.cy = (float)p[1];
+    f.cz = (float)p[2];
+    f.r2hi = std::max(f32_up(r2 * (1.0 + 4.0 * u)), 1e-30f);
+    f2.cchi = f32_up(cc * (1.0 + 1e-6));
+    f2.cc32 = (float)cc;
+    const double kd1 = u * (16.2 + 26.2 * 1.00001) * 1.01;  // primary rays: |o| = 0, |d|^2 <= 1.00001
+    f2.thrp = f32_up(((double)f.r2hi + kd1 * (double)f2.cchi) * (1.0 + 1e-6));
+    f2.pad = 0.0f;
+}
+
 // f64::to_radians (2017 std: self * (PI / 180)), then libm tan (ray.rs:45).
 double fov_adjustment(double fov) { return std::tan(fov * (3.14159265358979323846 / 180.0) / 2.0); }
 
@@ -78,6 +106,9 @@ RgKernelArgs make_args(const rg_scene *s) {
     std::memset(&a, 0, sizeof a);
     a.sph = s->sph;
     a.sph_cc = s->sph_cc;
+    a.sphf = s->sphf;
+    a.sphf2 = s->sphf2;
+    a.path = s->path;
     a.sph_id = s->sph_id;
     a.pln = s->pln;
     a.pln_id = s->pln_id;
@@ -96,9 +127,10 @@ RgKernelArgs make_args(const rg_scene *s) {
     a.n_bodies = s->n_bodies;
     a.n_lights = s->n_lights;
     a.n_textures = s->n_textures;
-    // LDS arena: [sph | cc (padded to 16 B) | bodies | mats | lights | texture descriptors]
+    // LDS arena: [sphf | sphf2 | sph | cc (padded to 16 B) | bodies | mats | lights | texture descriptors]
     auto al16 = [](uint32_t v) { return (v + 15u) & ~15u; };
-    a.lds_cc = (uint32_t)s->n_sph * (uint32_t)sizeof(RgSph);
+    a.lds_sph = (uint32_t)s->n_sph * (uint32_t)(sizeof(RgSphF) + sizeof(RgSphF2));
+    a.lds_cc = a.lds_sph + (uint32_t)s->n_sph * (uint32_t)sizeof(RgSph);
     a.lds_bodies = al16(a.lds_cc + (uint32_t)s->n_sph * 8u);
     a.lds_hot_bytes = a.lds_bodies;
     a.lds_mats = a.lds_bodies + (uint32_t)s->n_bodies * (uint32_t)sizeof(RgBodyDev);
@@ -187,6 +219,8 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
     if (!ok(hipSetDevice(device))) { release(s); return RG_ERR_DEVICE; }
 
     std::vector<RgSph> sph;
+    std::vector<RgSphF> sphf;
+    std::vector<RgSphF2> sphf2;
     std::vector<double> sph_cc;
     std::vector<int32_t> sph_id, pln_id, dsk_id, box_id;
     std::vector<RgPln> pln;
@@ -217,6 +251,9 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
             // r2 = radius * radius and cc = (c.c) evaluated exactly as the per-ray
             // reference expressions (bodies.rs:95,97) -> bit-identical.
             sph.push_back(RgSph{p[0], p[1], p[2], p[3] * p[3]});
+            sphf.emplace_back();
+            sphf2.emplace_back();
+            make_filter_records(p, sphf.back(), sphf2.back());
             sph_cc.push_back(dot3(p, p));  // padded to an even count after the loop
             sph_id.push_back((int32_t)i);
             break;
@@ -265,6 +302,8 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
     if (st == RG_OK) st = upload(s, &s->dst, vec.data(), vec.size())
     RG_UP(sph, sph);
     RG_UP(sph_cc, sph_cc);
+    RG_UP(sphf, sphf);
+    RG_UP(sphf2, sphf2);
     RG_UP(sph_id, sph_id);
     RG_UP(pln, pln);
     RG_UP(pln_id, pln_id);
@@ -444,6 +483,12 @@ rg_status rg_render_stream(const rg_scene *s, uint32_t width, uint32_t height, u
     }
     if (st == RG_OK && err_status != RG_OK) return err_status;
     return st;
+}
+
+rg_status rg_debug_set_path(rg_scene *s, int32_t path) {
+    if (!s || path < RG_PATH_AUTO || path > RG_PATH_HEAVY) return RG_ERR_INVALID_ARGUMENT;
+    s->path = path;
+    return RG_OK;
 }
 
 rg_status rg_trace(const rg_scene *s, const double *rays, uint32_t n, double *dist, int32_t *body) {

@@ -29,6 +29,10 @@ template <class T>
 __device__ __forceinline__ const RG_CONST T *rg_cptr(const T *p) { return (const RG_CONST T *)p; }
 
 struct alignas(16) RgSph { double cx, cy, cz, r2; };
+// f32 pre-filter records (see rg_kernels.hip, "f32 pre-filter"): conservative
+// bounds, never values the exact test uses.
+struct alignas(16) RgSphF { float cx, cy, cz, r2hi; };       // c rounded to f32; r2 rounded up (+slack)
+struct alignas(16) RgSphF2 { float cchi, thrp, cc32, pad; };  // |c|^2 rounded up; primary-ray threshold; fl32(c.c)
 struct alignas(16) RgPln { double ox, oy, oz, nx, ny, nz, on, pad; };
 struct alignas(16) RgDsk { double ox, oy, oz, nx, ny, nz, r, on; };
 struct alignas(16) RgBox { double lo[3], hi[3]; };
@@ -71,6 +75,8 @@ struct RgKernelArgs {
     // hot tables
     const RgSph *sph;
     const double *sph_cc;
+    const RgSphF *sphf;
+    const RgSphF2 *sphf2;
     const int32_t *sph_id;
     const RgPln *pln;
     const int32_t *pln_id;
@@ -86,7 +92,9 @@ struct RgKernelArgs {
     const RgTexDev *texs;
     int32_t n_bodies, n_lights, n_textures;
     // LDS arena (byte offsets; used by the LDS-staged kernel variants)
-    uint32_t lds_cc, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
+    // [sphf | sphf2 | sph | cc | bodies | mats | lights | texs]; lds_sph = start of the f64 sphere table
+    uint32_t lds_sph, lds_cc, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
+    int32_t path;            // RG_PATH_* forced by rg_debug_set_path, or RG_PATH_AUTO
     // frame
     uint32_t width, height;
     uint32_t tile_rows, tile_stride, tile_offset, out_rows;
@@ -99,6 +107,10 @@ struct RgKernelArgs {
     float *rgb;              // nullable, out_rows * width * 3
     unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=~error key [16+16q]=tile queue heads (RG_COUNTER_WORDS words)
 };
+
+#define RG_PATH_AUTO -1
+#define RG_PATH_LIGHT 0   // 2 waves/SIMD, batched shadow rays, exact f64 tests only
+#define RG_PATH_HEAVY 1   // 4 waves/SIMD, one ray per lane, f32 pre-filter + exact f64 tests
 
 #define RG_COUNTER_WORDS (16 + 16 * 16)  // stats + 16 queue heads, 128 B apart
 

@@ -145,18 +145,78 @@ __device__ __forceinline__ bool disk_hit(const RgDsk &k, V3 o, V3 d, double &t) 
 struct SphScalar {
     const RG_CONST RgSph *s;
     const RG_CONST double *cc;
+    const RG_CONST RgSphF *f;
+    const RG_CONST RgSphF2 *f2;
     __device__ __forceinline__ RgSph get(int i) const { return s[i]; }
     __device__ __forceinline__ double getcc(int i) const { return cc[i]; }
+    __device__ __forceinline__ RgSphF getf(int i) const { return f[i]; }
+    __device__ __forceinline__ RgSphF2 getf2(int i) const { return f2[i]; }
 };
 struct SphLds {
     const RgSph *s;
     const double *cc;
+    const RgSphF *f;
+    const RgSphF2 *f2;
     __device__ __forceinline__ RgSph get(int i) const { return s[i]; }
     __device__ __forceinline__ double getcc(int i) const { return cc[i]; }
+    __device__ __forceinline__ RgSphF getf(int i) const { return f[i]; }
+    __device__ __forceinline__ RgSphF2 getf2(int i) const { return f2[i]; }
 };
 
+// ---------------------------------------------------------------- f32 pre-filter
+// Heavy scenes first test every sphere in f32 (FMA allowed, 2 cycles per wave
+// instruction vs 4 for f64) against an INFLATED threshold, and run the exact
+// reference test (f64, unfused, bodies.rs:92-119) only for candidates, so the
+// accepted set and every distance are bit-identical to the reference.
+//
+// Bound (u = 2^-24, P_k = |c_k| + |o_k|, S_pp = sum P_k^2, S_p = sum P_k |d_k|):
+// with c, o, d rounded to f32, h = c - o, adj = h.d and hh = h.h as FMA chains
+// and opp = fma(-adj, adj, hh):
+//   |opp32 - OPP| <= u (8.002 S_pp + 13.004 S_p^2)   (f32 path, vs exact reals)
+//   |opp64 - OPP| <= 2^-53 (6.02 S_pp + 10.04 S_p^2) (the reference's f64 path)
+// and S_pp <= 2(|c|^2 + |o|^2), S_p^2 <= S_pp |d|^2, hence
+//   |opp32 - opp64| <= Kd (|c|^2 + |o|^2),  Kd = u (16.2 + 26.2 |d|^2) (rounded up, +1%).
+// "miss" is declared only if opp32 > r2hi + Kd(|c|^2 + |o|^2) with r2hi >= r2
+// (rounded up on the host with 4u slack, which also covers the two f32
+// roundings of the threshold), so opp64 > r2 there: the exact test would
+// reject too.  NaN/inf anywhere makes the comparison false -> candidate.
+struct RayF {
+    float ox, oy, oz, dx, dy, dz;
+    float kd;    // Kd for this ray
+    float kdo2;  // Kd * |o|^2 (rounded up)
+};
+__device__ __forceinline__ RayF make_rayf(V3 o, V3 d) {
+    RayF r;
+    r.ox = (float)o.x; r.oy = (float)o.y; r.oz = (float)o.z;
+    r.dx = (float)d.x; r.dy = (float)d.y; r.dz = (float)d.z;
+    const float d2 = (float)dot(d, d) * 1.000001f;   // >= |d|^2
+    const float o2 = (float)dot(o, o) * 1.000001f;   // >= |o|^2
+    r.kd = 5.9604645e-08f * (16.2f + 26.2f * d2) * 1.01f;
+    r.kdo2 = r.kd * o2 * 1.000001f;
+    return r;
+}
+// true: the exact test may accept this sphere (run it); false: certain miss
+__device__ __forceinline__ bool filter_general(const RgSphF &f, const RgSphF2 &f2, const RayF &r) {
+    const float hx = f.cx - r.ox, hy = f.cy - r.oy, hz = f.cz - r.oz;
+    const float adj = __builtin_fmaf(hz, r.dz, __builtin_fmaf(hy, r.dy, hx * r.dx));
+    const float hh = __builtin_fmaf(hz, hz, __builtin_fmaf(hy, hy, hx * hx));
+    const float opp = __builtin_fmaf(-adj, adj, hh);
+    const float thr = __builtin_fmaf(r.kd, f2.cchi, f.r2hi + r.kdo2);
+    return !(opp > thr);
+}
+// primary rays: o = 0 and |d|^2 <= 1.00001, so the threshold is a per-sphere
+// constant (thrp, host-precomputed) and h.h = fl32(c.c) (cc32)
+__device__ __forceinline__ bool filter_primary(const RgSphF &f, const RgSphF2 &f2, float dx, float dy, float dz) {
+    const float adj = __builtin_fmaf(f.cz, dz, __builtin_fmaf(f.cy, dy, f.cx * dx));
+    const float opp = __builtin_fmaf(-adj, adj, f2.cc32);
+    return !(opp > f2.thrp);
+}
+
 #ifndef RG_SPH_GROUP
-#define RG_SPH_GROUP 2   // spheres per miss-test group (one divergent branch per group)
+#define RG_SPH_GROUP 2     // spheres per exact miss-test group (one divergent branch per group)
+#endif
+#ifndef RG_FILTER_GROUP
+#define RG_FILTER_GROUP 4  // spheres per f32-filter group
 #endif
 
 // Primary rays start at the origin (ray.rs:53): h = c - 0 = c exactly, so
@@ -185,8 +245,43 @@ __device__ __forceinline__ void sph_primary_group(const RgKernelArgs &a, const S
     }
 }
 
-template <class Src>
+// f32-filtered primary group: exact f64 work only for candidate spheres
+template <int G, class Src>
+__device__ __forceinline__ void sph_primary_group_f(const RgKernelArgs &a, const Src &src, int i, V3 d, float dx,
+                                                    float dy, float dz, Closest &c) {
+    bool cand[G];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        cand[k] = filter_primary(src.getf(i + k), src.getf2(i + k), dx, dy, dz);
+        any |= cand[k];
+    }
+    if (any) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            if (cand[k]) {
+                const RgSph s = src.get(i + k);
+                const double cc = src.getcc(i + k);
+                const double adj = (s.cx * d.x + s.cy * d.y) + s.cz * d.z;
+                const double opp = cc - adj * adj;
+                double t;
+                if (!(opp > s.r2) && sphere_tail(s.r2, opp, adj, t)) closest_add(c, t, rg_cptr(a.sph_id)[i + k]);
+            }
+        }
+    }
+}
+
+template <bool F32F, class Src>
 __device__ __forceinline__ void sph_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
+    if constexpr (F32F) {
+        constexpr int G = RG_FILTER_GROUP;
+        const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+        const int n = a.n_sph, nfull = n - n % G;
+        int i = 0;
+        for (; i < nfull; i += G) sph_primary_group_f<G>(a, src, i, d, dx, dy, dz, c);
+        for (; i < n; ++i) sph_primary_group_f<1>(a, src, i, d, dx, dy, dz, c);
+        return;
+    }
     constexpr int G = RG_SPH_GROUP;
     const int n = a.n_sph, nfull = n - n % G;
     int i = 0;
@@ -227,9 +322,53 @@ __device__ __forceinline__ void sph_query_group(const RgKernelArgs &a, const Src
     }
 }
 
-template <class Src>
+template <int G, class Src>
+__device__ __forceinline__ void sph_query_group_f(const RgKernelArgs &a, const Src &src, int i, V3 o, V3 d,
+                                                  const RayF &rf, bool shadow, double ld, Closest &c, bool &occl,
+                                                  bool &need) {
+    bool cand[G];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        cand[k] = filter_general(src.getf(i + k), src.getf2(i + k), rf) && need;
+        any |= cand[k];
+    }
+    if (any) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            if (cand[k]) {
+                const RgSph s = src.get(i + k);
+                const double hx = s.cx - o.x, hy = s.cy - o.y, hz = s.cz - o.z;
+                const double adj = (hx * d.x + hy * d.y) + hz * d.z;
+                const double opp = ((hx * hx + hy * hy) + hz * hz) - adj * adj;
+                double t;
+                if (!(opp > s.r2) && sphere_tail(s.r2, opp, adj, t)) {
+                    if (shadow) {
+                        if (!(t > ld)) { occl = true; need = false; }
+                    } else {
+                        closest_add(c, t, rg_cptr(a.sph_id)[i + k]);
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <bool F32F, class Src>
 __device__ __forceinline__ bool sph_query(const RgKernelArgs &a, const Src &src, V3 o, V3 d, bool shadow, double ld,
                                           Closest &c, bool &occl, bool &need) {
+    if constexpr (F32F) {
+        constexpr int G = RG_FILTER_GROUP;
+        const RayF rf = make_rayf(o, d);
+        const int n = a.n_sph, nfull = n - n % G;
+        int i = 0;
+        for (; i < nfull; i += G) {
+            sph_query_group_f<G>(a, src, i, o, d, rf, shadow, ld, c, occl, need);
+            if (((i / G) & 3) == 3 && !__any(need)) return false;
+        }
+        for (; i < n; ++i) sph_query_group_f<1>(a, src, i, o, d, rf, shadow, ld, c, occl, need);
+        return __any(need);
+    }
     constexpr int G = RG_SPH_GROUP;
     const int n = a.n_sph, nfull = n - n % G;
     int i = 0;
@@ -241,9 +380,9 @@ __device__ __forceinline__ bool sph_query(const RgKernelArgs &a, const Src &src,
     return __any(need);
 }
 
-template <class Src>
+template <bool F32F, class Src>
 __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
-    sph_primary(a, src, d, c);
+    sph_primary<F32F>(a, src, d, c);
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = rg_cptr(a.pln)[i];
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137
@@ -274,12 +413,12 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
 // !(t > light_distance)  <=>  !(min t > light_distance)  (rendering.rs:152-155),
 // so a lane stops testing at its first such hit and the wave leaves the body
 // loops as soon as every lane that is still testing is a finished shadow ray.
-template <class Src>
+template <bool F32F, class Src>
 __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &src, const Ray &r, bool shadow, double ld,
                                             Closest &c, bool &occl) {
     const V3 o = r.o, d = r.d;
     bool need = true;
-    if (!sph_query(a, src, o, d, shadow, ld, c, occl, need)) return;
+    if (!sph_query<F32F>(a, src, o, d, shadow, ld, c, occl, need)) return;
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = rg_cptr(a.pln)[i];
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137-148
@@ -614,19 +753,25 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // repeatedly takes the next 8x8 pixel tile from an atomic queue
 // (counters[16..], sharded) and runs the per-lane state machine until its 64 lanes have
 // written their pixels.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB>
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F>
 __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     typename std::conditional<LSPH, SphLds, SphScalar>::type src;
     Cold T;
     if constexpr (LSPH) {
-        stage16(smem, a.sph, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSph));
+        stage16(smem, a.sphf, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF));
+        stage16(smem + (size_t)a.n_sph * sizeof(RgSphF), a.sphf2, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF2));
+        stage16(smem + a.lds_sph, a.sph, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSph));
         stage16(smem + a.lds_cc, a.sph_cc, a.lds_bodies - a.lds_cc);
-        src.s = reinterpret_cast<const RgSph *>(smem);
+        src.f = reinterpret_cast<const RgSphF *>(smem);
+        src.f2 = reinterpret_cast<const RgSphF2 *>(smem + (size_t)a.n_sph * sizeof(RgSphF));
+        src.s = reinterpret_cast<const RgSph *>(smem + a.lds_sph);
         src.cc = reinterpret_cast<const double *>(smem + a.lds_cc);
     } else {
         src.s = rg_cptr(a.sph);
         src.cc = rg_cptr(a.sph_cc);
+        src.f = rg_cptr(a.sphf);
+        src.f2 = rg_cptr(a.sphf2);
     }
     if constexpr (LCOLD) {
         stage16(smem + a.lds_bodies, a.bodies, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgBodyDev));
@@ -718,7 +863,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             q.o = v3(0.0, 0.0, 0.0);
             q.d = normalize(v3(sx, sy, -1.0));
             n_prim++;
-            trace_primary(a, src, q.d, c);
+            trace_primary<F32F>(a, src, q.d, c);
             mode = MODE_CLOSEST;
             qdepth = 0;
         }
@@ -892,7 +1037,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                     Ray r1;
                     r1.o = q.o;
                     r1.d = mode == MODE_SHADOW ? sb.d[0] : q.d;
-                    trace_query(a, src, r1, mode == MODE_SHADOW, sb.ld[0], c, o1);
+                    trace_query<F32F>(a, src, r1, mode == MODE_SHADOW, sb.ld[0], c, o1);
                     occl = o1 ? 1u : 0u;
                 }
             } else {
@@ -901,7 +1046,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                 if (mode == MODE_CLOSEST) {
 #ifndef RG_DBG_NO_SEC_TRACE
                     bool unused = false;
-                    trace_query(a, src, q, false, 0.0, c, unused);
+                    trace_query<F32F>(a, src, q, false, 0.0, c, unused);
 #endif
                 }
                 if (mode == MODE_SHADOW) {
@@ -940,8 +1085,9 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
     closest_init(c);
     bool occl = false;
     if (alive) {
-        SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc)};
-        trace_query(a, src, r, false, 0.0, c, occl);
+        SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc), rg_cptr(a.sphf), rg_cptr(a.sphf2)};
+        if (a.path == RG_PATH_HEAVY) trace_query<true>(a, src, r, false, 0.0, c, occl);
+        else trace_query<false>(a, src, r, false, 0.0, c, occl);
         if (c.nan && c.nhit >= 2) raise_error(a, i, RG_ERR_NAN_DISTANCE);
         dist[i] = c.id >= 0 ? c.t : 0.0;
         body[i] = c.id;
@@ -951,11 +1097,11 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
 // ---------------------------------------------------------------- launchers
 // One persistent block per CU slot: grid = CUs x (blocks per CU the register
 // and LDS budgets admit), capped by the tiles the frame has.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB>
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F>
 static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream) {
     static int cus = 0, per_cu = 0;
     static size_t lds_cached = ~(size_t)0;
-    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB>;
+    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F>;
     if (cus == 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
@@ -983,17 +1129,20 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
 #ifndef RG_LDS_BUDGET
 #define RG_LDS_BUDGET (160 * 1024)       // one block per CU owns the CU's LDS
 #endif
+#ifndef RG_HEAVY_F32_FILTER
+#define RG_HEAVY_F32_FILTER true  // heavy path: f32 pre-filter in front of the exact sphere tests
+#endif
 #ifndef RG_HEAVY_SCENE_BODIES
 #define RG_HEAVY_SCENE_BODIES 32         // bodies per ray at which the trace loop, not shading, dominates
 #endif
 
-template <int MAXD, int WPS, int LB>
+template <int MAXD, int WPS, int LB, bool F32F>
 static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream) {
     if (a->lds_total_bytes <= RG_LDS_BUDGET)  // whole scene (empty sphere part if n_sph == 0)
-        return launch_one<MAXD, true, true, WPS, LB>(a, a->lds_total_bytes, stream);
+        return launch_one<MAXD, true, true, WPS, LB, F32F>(a, a->lds_total_bytes, stream);
     if (a->n_sph > 0 && a->lds_hot_bytes <= RG_LDS_BUDGET)
-        return launch_one<MAXD, true, false, WPS, LB>(a, a->lds_hot_bytes, stream);
-    return launch_one<MAXD, false, false, WPS, LB>(a, 0, stream);
+        return launch_one<MAXD, true, false, WPS, LB, F32F>(a, a->lds_hot_bytes, stream);
+    return launch_one<MAXD, false, false, WPS, LB, F32F>(a, 0, stream);
 }
 
 template <int MAXD>
@@ -1002,12 +1151,12 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
     // fatter iterations (RG_LB shadow rays per pass) at 2 waves/SIMD.  Heavy
     // scenes: the body loop dominates and waves mix ray kinds -> one ray per
     // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
+    bool heavy = a->n_sph + a->n_pln + a->n_dsk + a->n_box >= RG_HEAVY_SCENE_BODIES;
 #if defined(RG_FORCE_WPS)
-    const bool heavy = RG_FORCE_WPS == 4;
-#else
-    const bool heavy = a->n_sph + a->n_pln + a->n_dsk + a->n_box >= RG_HEAVY_SCENE_BODIES;
+    heavy = RG_FORCE_WPS == 4;
 #endif
-    return heavy ? launch_waves<MAXD, 4, 1>(a, stream) : launch_waves<MAXD, 2, RG_LB>(a, stream);
+    if (a->path != RG_PATH_AUTO) heavy = a->path == RG_PATH_HEAVY;
+    return heavy ? launch_waves<MAXD, 4, 1, RG_HEAVY_F32_FILTER>(a, stream) : launch_waves<MAXD, 2, RG_LB, false>(a, stream);
 }
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {

@@ -363,12 +363,14 @@ class SceneDesc:
 class DeviceScene:
     """An rg_scene handle: the scene uploaded to one GPU."""
 
-    def __init__(self, scene: "Scene", device: int = 0):
+    def __init__(self, scene: "Scene", device: int = 0, path: Optional[int] = None):
         self._desc = SceneDesc(scene)
         h = C.c_void_p()
         _abi.check(_abi.lib().rg_scene_create(self._desc.ptr(), int(device), C.byref(h)), "rg_scene_create")
         self.handle = h
         self.device = device
+        if path is not None:
+            self.set_path(path)
 
     def close(self) -> None:
         if getattr(self, "handle", None):
@@ -380,6 +382,10 @@ class DeviceScene:
             self.close()
         except Exception:
             pass
+
+    def set_path(self, path: int) -> None:
+        """Force a kernel path (_abi.PATH_AUTO / PATH_LIGHT / PATH_HEAVY; include/raingun_debug.h)."""
+        _abi.check(_abi.lib().rg_debug_set_path(self.handle, int(path)))
 
     def set_max_depth(self, depth: int) -> None:
         _abi.check(_abi.lib().rg_scene_set_max_depth(self.handle, int(depth)))

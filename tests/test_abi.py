@@ -8,11 +8,12 @@ import pytest
 
 from raingun_amd import _abi
 
-HEADER = Path(__file__).resolve().parent.parent / "include" / "raingun.h"
+INCLUDE = Path(__file__).resolve().parent.parent / "include"
+HEADER = INCLUDE / "raingun.h"
 
 
-def declared_functions():
-    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+def declared_functions(header=HEADER):
+    text = re.sub(r"/\*.*?\*/", "", header.read_text(), flags=re.S)
     names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\**\s*(rg_[a-z0-9_]+)\s*\(", text, flags=re.M)
     return sorted(set(names))
 
@@ -26,13 +27,15 @@ def libpath():
 
 def test_header_matches_binding_table():
     assert declared_functions() == sorted(_abi.EXPORTED_SYMBOLS)
+    assert declared_functions(INCLUDE / "raingun_debug.h") == sorted(_abi.DEBUG_SYMBOLS)
 
 
 def test_library_exports_every_symbol(libpath):
     out = subprocess.run(["nm", "-D", "--defined-only", str(libpath)], capture_output=True, text=True,
                          check=True).stdout
     exported = {l.split()[-1] for l in out.splitlines() if l.strip()}
-    missing = [s for s in declared_functions() if s not in exported]
+    declared = declared_functions() + declared_functions(INCLUDE / "raingun_debug.h")
+    missing = [s for s in declared if s not in exported]
     assert not missing, missing
 
 

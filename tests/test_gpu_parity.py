@@ -26,9 +26,9 @@ def _device():
     assert lib.rg_device_count() > 0, "no HIP device visible"
 
 
-def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0):
+def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0, path=None):
     desc = SceneDesc(scene)
-    ds = DeviceScene(scene)
+    ds = DeviceScene(scene, path=path)
     st = _abi.rg_stats()
     g_rgba, g_rgb = ds.render_tiles(w, h, tile_rows, stride, offset, want_rgb=True, stats=st)
     o_st, o_rgba, o_rgb, o_counts, o_err = oracle_lib.render(desc, w, h, tile_rows, stride, offset, want_rgb=True)
@@ -42,9 +42,13 @@ def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0):
     return st
 
 
+PATHS = [_abi.PATH_LIGHT, _abi.PATH_HEAVY]  # both kernel paths on every scene
+
+
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", ["test1", "test2", "test3"])
-def test_examples_800x600(oracle_lib, example_scenes, name):
-    st = _compare(oracle_lib, example_scenes[name], 800, 600)
+def test_examples_800x600(oracle_lib, example_scenes, name, path):
+    st = _compare(oracle_lib, example_scenes[name], 800, 600, path=path)
     assert st.rays.primary == 800 * 600
 
 
@@ -67,8 +71,9 @@ def test_config3_test3_4k(oracle_lib, example_scenes):
     (200, 2, 2, 160, 90),
     (40, 4, 20, 160, 90),
 ])
-def test_synthetic(oracle_lib, n, planes, depth, w, h):
-    _compare(oracle_lib, synthetic_scene(n, planes, depth), w, h)
+@pytest.mark.parametrize("path", PATHS)
+def test_synthetic(oracle_lib, n, planes, depth, w, h, path):
+    _compare(oracle_lib, synthetic_scene(n, planes, depth), w, h, path=path)
 
 
 def test_odd_sizes_and_square(oracle_lib, example_scenes):
@@ -161,3 +166,45 @@ def test_aabb_normal_error_matches_oracle(oracle_lib):
     assert o_st == _abi.RG_ERR_AABB_NORMAL
     assert ei.value.status == o_st
     assert st.error_pixel == o_err
+
+
+@pytest.mark.parametrize("scale", [1.0, 40.0, 3000.0])
+def test_f32_prefilter_tangent_rays(oracle_lib, scale):
+    """Rays grazing sphere silhouettes (opp within 1e-9 relative of r^2), from
+    near and far origins at several scene scales: the heavy path's f32
+    pre-filter must never reject a sphere the exact f64 test accepts."""
+    from raingun_amd.color import Color
+    from raingun_amd.scene import Material, Sphere
+    rng = np.random.default_rng(11)
+    m = Material(Color.from_str("#ffffff"), 0.5)
+    centers = rng.uniform(-1, 1, size=(64, 3)) * scale * 4 + np.array([0, 0, -8 * scale])
+    radii = rng.uniform(0.01, 0.2, size=64) * scale
+    s = Scene(bodies=[Sphere(tuple(c), float(r), m) for c, r in zip(centers, radii)])
+    rays, targets = [], []
+    for _ in range(8192):
+        k = rng.integers(64)
+        c, r = centers[k], radii[k]
+        o = rng.uniform(-3, 3, size=3) * scale
+        d = c - o                                   # aim at the centre ...
+        perp = np.cross(d, rng.normal(size=3))
+        perp /= np.linalg.norm(perp)
+        o = o + perp * r * (1.0 + rng.uniform(-1e-9, 1e-9))  # ... then slide off by ~r, across d
+        if rng.integers(2):
+            d /= np.linalg.norm(d)
+        rays.append(np.concatenate([o, d]))
+        targets.append(k)
+    rays, targets = np.array(rays), np.array(targets)
+    for path in PATHS:
+        ds = DeviceScene(s, path=path)
+        gd, gb = ds.trace(rays)
+        ds.close()
+        st, od, ob = oracle_lib.trace(SceneDesc(s), rays)
+        assert st == 0
+        assert np.array_equal(gb, ob), f"path {path}: {np.count_nonzero(gb != ob)} rays differ"
+        hit = ob >= 0
+        assert np.array_equal(gd[hit], od[hit])
+    # where nothing else is in the way, grazing rays split between hitting and
+    # missing their target: the boundary really is exercised
+    own = (ob == targets) | (ob == -1)
+    assert own.sum() > 1000
+    assert 0.2 < (ob[own] == targets[own]).mean() < 0.8
