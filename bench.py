@@ -127,39 +127,21 @@ def load_traffic(workload: str, n_gpus: int):
         return None
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="test1", help="test1 | test3 | synth<N>")
-    ap.add_argument("--width", type=int, default=3840)
-    ap.add_argument("--height", type=int, default=2160)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
-
+def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cpu: bool):
+    """Time `args.steps` frames of `workload` on this rank (after `args.warmup`),
+    frame sharded over `world` ranks and gathered to rank 0.  Returns the
+    rank-0 result dict (None on other ranks)."""
     import torch
     import torch.distributed as dist
 
     from raingun_amd import _abi
+    from raingun_amd import distributed as rd
     from raingun_amd.scene import DeviceScene
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local_rank)
-
-    scene, label, src, body_counts, ops_per_ray = load_workload(args.workload)
+    scene, label, src, body_counts, ops_per_ray = load_workload(workload)
     W, H = args.width, args.height
     ds = DeviceScene(scene, device=local_rank)  # scene + textures uploaded once, resident in HBM
     lib = _abi.lib()
-
-    from raingun_amd import distributed as rd
 
     tiling = rd.tiling(rank, world, TILE_ROWS)
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
@@ -170,7 +152,8 @@ def main() -> None:
 
     stream = torch.cuda.current_stream(dev)
     sh = C.c_void_p(stream.cuda_stream)
-    events = []  # (start, end) around each timed launch, on the render stream
+    events = []          # (start, end) around each timed launch, on the render stream
+    max_events = [0]
 
     def render(stats=None):
         st = lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(out.data_ptr()), None, sh,
@@ -178,17 +161,15 @@ def main() -> None:
         _abi.check(st, "rg_render_tiles_async")
 
     def render_tiles(_t):
-        if events is not None and len(events) < max_events[0]:
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
+        if len(events) < max_events[0]:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
             render()
-            b.record(stream)
-            events.append((a, b))
+            e1.record(stream)
+            events.append((e0, e1))
         else:
             render()
         return out
-
-    max_events = [0]
 
     def step():
         rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
@@ -219,67 +200,111 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in events) / len(events)
+    kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / len(events)
 
-    tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms_max = float(tt[0]), float(tt[1])
+    elapsed = float(tt[0])
+    ds.close()
+    if rank != 0:
+        return None
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = rays_per_frame * args.steps / elapsed / 1e6
+    my_rays = stats.rays.primary + stats.rays.shadow + stats.rays.secondary
+    ops = my_rays * ops_per_ray
+    achieved_t = ops / (kernel_ms * 1e-3) / 1e12
+    alg_bytes = my_rows * W * 4  # framebuffer written once; scene/texture reads are cache-resident re-reads
+    tex = texture_bytes(scene)
+    traffic = load_traffic(workload, world)
+    res = {
+        "value": round(value, 3),
+        "ms_per_step": round(ms_per_step, 4),
+        "kernel_ms": round(kernel_ms, 4),
+        "data": src,
+        "config": {"workload": label, "width": W, "height": H, "max_recursion_depth": scene.max_recursion_depth,
+                   "bodies": body_counts, "lights": len(scene.lights), "tile_rows": TILE_ROWS,
+                   "parallelism": f"row-tiles x{world} (round-robin 16-row tiles, RCCL gather to rank 0)"},
+        "rays_per_frame": {"primary": rays[0], "shadow": rays[1], "secondary": rays[2], "total": rays_per_frame},
+        "roofline": {
+            "bound": "valu_fp64",
+            "achieved": round(achieved_t, 4),
+            "peak": FP64_PEAK_TOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_t / FP64_PEAK_TOPS, 5),
+            "traffic": traffic,
+            "basis": f"reference-equivalent work: {ops_per_ray} FP64 ops per ray (16/sphere, 14/plane, 20/disk, "
+                     f"18/aabb; SURVEY.md 8d) x {my_rays} rays per launch / mean rg_render_kernel time (HIP events "
+                     f"on the render stream). On >=32-body scenes the kernel's f32 pre-filter skips most of that "
+                     f"FP64 work exactly, so frac can exceed 1 there",
+        },
+        "roofline_hbm": {
+            "bound": "hbm",
+            "achieved": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 3),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(alg_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),
+            "traffic": traffic,
+            "basis": f"{alg_bytes} B framebuffer written per launch (+{tex} B of textures, L2/MALL resident)",
+        },
+    }
+    if cpu:
+        res["cpu_baseline"] = cpu_baseline(scene, W, H)
+        res["gpu_over_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
+    return res
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="test1", help="test1 | test3 | synth<N>")
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="skip the extra north_star line item (1024 spheres, 3840x2160, depth 5)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local_rank)
+    cpu = (not args.no_cpu_baseline) and world == 1
+
+    main_res = measure(args.workload, args, world, rank, local_rank, dev, cpu)
+    ns_res = None
+    if not args.no_north_star and args.workload != "synth1024":
+        ns_res = measure("synth1024", args, world, rank, local_rank, dev, cpu)
 
     if rank == 0:
-        ms_per_step = elapsed * 1e3 / args.steps
-        value = rays_per_frame * args.steps / elapsed / 1e6
-        # roofline of the dominant kernel (rg_render_kernel) on this rank
-        my_rays = stats.rays.primary + stats.rays.shadow + stats.rays.secondary
-        ops = my_rays * ops_per_ray
-        achieved_t = ops / (kernel_ms * 1e-3) / 1e12
-        out_bytes = my_rows * W * 4
-        tex = texture_bytes(scene)
-        alg_bytes = out_bytes  # framebuffer written once; scene/texture reads are cache-resident re-reads
-        traffic = load_traffic(args.workload, world)
         line = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": main_res["value"],
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": src,
-            "config": {"workload": label, "width": W, "height": H, "max_recursion_depth": scene.max_recursion_depth,
-                       "bodies": body_counts, "lights": len(scene.lights), "tile_rows": TILE_ROWS,
-                       "parallelism": f"row-tiles x{world} (round-robin 16-row tiles, RCCL gather to rank 0)"},
-            "rays_per_frame": {"primary": rays[0], "shadow": rays[1], "secondary": rays[2], "total": rays_per_frame},
-            "kernel_ms": round(kernel_ms, 4),
-            "roofline": {
-                "bound": "valu_fp64",
-                "achieved": round(achieved_t, 4),
-                "peak": FP64_PEAK_TOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved_t / FP64_PEAK_TOPS, 5),
-                "traffic": traffic,
-                "basis": f"{ops_per_ray} algorithmic FP64 ops per ray (16/sphere, 14/plane, 20/disk, 18/aabb) x "
-                         f"{my_rays} rays per launch / mean rg_render_kernel time from HIP events on the render stream",
-            },
-            "roofline_hbm": {
-                "bound": "hbm",
-                "achieved": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 3),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(alg_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),
-                "traffic": traffic,
-                "basis": f"{alg_bytes} B framebuffer written per launch (+{tex} B of textures, L2/MALL resident)",
-            },
         }
-        if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(scene, W, H)
-            line["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
+        line.update({k: v for k, v in main_res.items() if k not in ("value", "ms_per_step")})
+        if ns_res is not None:
+            line["north_star_1024_spheres"] = ns_res
         print(json.dumps(line), flush=True)
-    ds.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -127,11 +127,14 @@ RgKernelArgs make_args(const rg_scene *s) {
     a.n_bodies = s->n_bodies;
     a.n_lights = s->n_lights;
     a.n_textures = s->n_textures;
-    // LDS arena: [sphf | sphf2 | sph | cc (padded to 16 B) | bodies | mats | lights | texture descriptors]
+    // LDS arena: [sphf | sphf2 | sph | cc (padded to 16 B) | pln | dsk | box (padded) | bodies | mats | lights | texs]
     auto al16 = [](uint32_t v) { return (v + 15u) & ~15u; };
     a.lds_sph = (uint32_t)s->n_sph * (uint32_t)(sizeof(RgSphF) + sizeof(RgSphF2));
     a.lds_cc = a.lds_sph + (uint32_t)s->n_sph * (uint32_t)sizeof(RgSph);
-    a.lds_bodies = al16(a.lds_cc + (uint32_t)s->n_sph * 8u);
+    a.lds_pln = al16(a.lds_cc + (uint32_t)s->n_sph * 8u);
+    a.lds_dsk = a.lds_pln + (uint32_t)s->n_pln * (uint32_t)sizeof(RgPln);
+    a.lds_box = a.lds_dsk + (uint32_t)s->n_dsk * (uint32_t)sizeof(RgDsk);
+    a.lds_bodies = al16(a.lds_box + (uint32_t)s->n_box * (uint32_t)sizeof(RgBox));
     a.lds_hot_bytes = a.lds_bodies;
     a.lds_mats = a.lds_bodies + (uint32_t)s->n_bodies * (uint32_t)sizeof(RgBodyDev);
     a.lds_lights = al16(a.lds_mats + (uint32_t)s->n_bodies * (uint32_t)sizeof(RgMatDev));

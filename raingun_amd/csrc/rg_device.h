@@ -92,8 +92,8 @@ struct RgKernelArgs {
     const RgTexDev *texs;
     int32_t n_bodies, n_lights, n_textures;
     // LDS arena (byte offsets; used by the LDS-staged kernel variants)
-    // [sphf | sphf2 | sph | cc | bodies | mats | lights | texs]; lds_sph = start of the f64 sphere table
-    uint32_t lds_sph, lds_cc, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
+    // [sphf | sphf2 | sph | cc | pln | dsk | box | bodies | mats | lights | texs] (byte offsets)
+    uint32_t lds_sph, lds_cc, lds_pln, lds_dsk, lds_box, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
     int32_t path;            // RG_PATH_* forced by rg_debug_set_path, or RG_PATH_AUTO
     // frame
     uint32_t width, height;

@@ -147,6 +147,12 @@ struct SphScalar {
     const RG_CONST double *cc;
     const RG_CONST RgSphF *f;
     const RG_CONST RgSphF2 *f2;
+    const RG_CONST RgPln *pl;
+    const RG_CONST RgDsk *dk;
+    const RG_CONST RgBox *bx;
+    __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
+    __device__ __forceinline__ RgDsk getd(int i) const { return dk[i]; }
+    __device__ __forceinline__ RgBox getb(int i) const { return bx[i]; }
     __device__ __forceinline__ RgSph get(int i) const { return s[i]; }
     __device__ __forceinline__ double getcc(int i) const { return cc[i]; }
     __device__ __forceinline__ RgSphF getf(int i) const { return f[i]; }
@@ -157,6 +163,12 @@ struct SphLds {
     const double *cc;
     const RgSphF *f;
     const RgSphF2 *f2;
+    const RgPln *pl;
+    const RgDsk *dk;
+    const RgBox *bx;
+    __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
+    __device__ __forceinline__ RgDsk getd(int i) const { return dk[i]; }
+    __device__ __forceinline__ RgBox getb(int i) const { return bx[i]; }
     __device__ __forceinline__ RgSph get(int i) const { return s[i]; }
     __device__ __forceinline__ double getcc(int i) const { return cc[i]; }
     __device__ __forceinline__ RgSphF getf(int i) const { return f[i]; }
@@ -249,17 +261,16 @@ __device__ __forceinline__ void sph_primary_group(const RgKernelArgs &a, const S
 template <int G, class Src>
 __device__ __forceinline__ void sph_primary_group_f(const RgKernelArgs &a, const Src &src, int i, V3 d, float dx,
                                                     float dy, float dz, Closest &c) {
-    bool cand[G];
+    // the group's filter results are OR-ed into one lane predicate (lane masks
+    // stay in SGPRs); the rare candidate branch re-evaluates the filter per
+    // sphere instead of keeping G per-lane flags alive
     bool any = false;
 #pragma unroll
-    for (int k = 0; k < G; ++k) {
-        cand[k] = filter_primary(src.getf(i + k), src.getf2(i + k), dx, dy, dz);
-        any |= cand[k];
-    }
+    for (int k = 0; k < G; ++k) any |= filter_primary(src.getf(i + k), src.getf2(i + k), dx, dy, dz);
     if (any) {
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            if (cand[k]) {
+            if (filter_primary(src.getf(i + k), src.getf2(i + k), dx, dy, dz)) {
                 const RgSph s = src.get(i + k);
                 const double cc = src.getcc(i + k);
                 const double adj = (s.cx * d.x + s.cy * d.y) + s.cz * d.z;
@@ -326,17 +337,13 @@ template <int G, class Src>
 __device__ __forceinline__ void sph_query_group_f(const RgKernelArgs &a, const Src &src, int i, V3 o, V3 d,
                                                   const RayF &rf, bool shadow, double ld, Closest &c, bool &occl,
                                                   bool &need) {
-    bool cand[G];
     bool any = false;
 #pragma unroll
-    for (int k = 0; k < G; ++k) {
-        cand[k] = filter_general(src.getf(i + k), src.getf2(i + k), rf) && need;
-        any |= cand[k];
-    }
-    if (any) {
+    for (int k = 0; k < G; ++k) any |= filter_general(src.getf(i + k), src.getf2(i + k), rf);
+    if (any && need) {
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            if (cand[k]) {
+            if (need && filter_general(src.getf(i + k), src.getf2(i + k), rf)) {
                 const RgSph s = src.get(i + k);
                 const double hx = s.cx - o.x, hy = s.cy - o.y, hz = s.cz - o.z;
                 const double adj = (hx * d.x + hy * d.y) + hz * d.z;
@@ -384,7 +391,7 @@ template <bool F32F, class Src>
 __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
     sph_primary<F32F>(a, src, d, c);
     for (int i = 0; i < a.n_pln; ++i) {
-        const RgPln p = rg_cptr(a.pln)[i];
+        const RgPln p = src.getp(i);
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137
         if (den > 1e-6) {
             double dist = p.on / den;                           // v = o_p - 0 = o_p: v.n = o.n
@@ -393,7 +400,7 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
     }
     const V3 o = v3(0.0, 0.0, 0.0);
     for (int i = 0; i < a.n_dsk; ++i) {
-        const RgDsk k = rg_cptr(a.dsk)[i];
+        const RgDsk k = src.getd(i);
         double t;
         if (disk_hit(k, o, d, t)) closest_add(c, t, rg_cptr(a.dsk_id)[i]);
     }
@@ -401,7 +408,7 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
         V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);           // ray.rs:24
         int sx = inv.x < 0.0, sy = inv.y < 0.0, sz = inv.z < 0.0;
         for (int i = 0; i < a.n_box; ++i) {
-            const RgBox b = rg_cptr(a.box)[i];
+            const RgBox b = src.getb(i);
             double t;
             if (aabb_hit(b, o, inv, sx, sy, sz, t)) closest_add(c, t, rg_cptr(a.box_id)[i]);
         }
@@ -420,7 +427,7 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
     bool need = true;
     if (!sph_query<F32F>(a, src, o, d, shadow, ld, c, occl, need)) return;
     for (int i = 0; i < a.n_pln; ++i) {
-        const RgPln p = rg_cptr(a.pln)[i];
+        const RgPln p = src.getp(i);
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137-148
         if (den > 1e-6 && need) {
             double vx = p.ox - o.x, vy = p.oy - o.y, vz = p.oz - o.z;
@@ -436,7 +443,7 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
     }
     if (!__any(need)) return;
     for (int i = 0; i < a.n_dsk; ++i) {
-        const RgDsk k = rg_cptr(a.dsk)[i];
+        const RgDsk k = src.getd(i);
         double t;
         if (need && disk_hit(k, o, d, t)) {
             if (shadow) {
@@ -450,7 +457,7 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
         V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
         int sx = inv.x < 0.0, sy = inv.y < 0.0, sz = inv.z < 0.0;
         for (int i = 0; i < a.n_box; ++i) {
-            const RgBox b = rg_cptr(a.box)[i];
+            const RgBox b = src.getb(i);
             double t;
             if (need && aabb_hit(b, o, inv, sx, sy, sz, t)) {
                 if (shadow) {
@@ -525,7 +532,7 @@ __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &s
     }
     if (!__any(occl != full)) return;
     for (int i = 0; i < a.n_pln; ++i) {
-        const RgPln p = rg_cptr(a.pln)[i];
+        const RgPln p = src.getp(i);
         const double vx = p.ox - o.x, vy = p.oy - o.y, vz = p.oz - o.z;     // bodies.rs:139
         const double num = (vx * p.nx + vy * p.ny) + vz * p.nz;             // :140 numerator
 #pragma unroll
@@ -545,7 +552,7 @@ __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &s
     }
     if (!__any(occl != full)) return;
     for (int i = 0; i < a.n_dsk; ++i) {
-        const RgDsk k = rg_cptr(a.dsk)[i];
+        const RgDsk k = src.getd(i);
 #pragma unroll
         for (int l = 0; l < LB; ++l) {
             double t;
@@ -559,7 +566,7 @@ __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &s
             const V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
             const int sx = inv.x < 0.0, sy = inv.y < 0.0, sz = inv.z < 0.0;
             for (int i = 0; i < a.n_box; ++i) {
-                const RgBox b = rg_cptr(a.box)[i];
+                const RgBox b = src.getb(i);
                 double t;
                 if (!((occl >> l) & 1u) && aabb_hit(b, o, inv, sx, sy, sz, t) && !(t > sb.ld[l])) occl |= 1u << l;
             }
@@ -762,16 +769,25 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         stage16(smem, a.sphf, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF));
         stage16(smem + (size_t)a.n_sph * sizeof(RgSphF), a.sphf2, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF2));
         stage16(smem + a.lds_sph, a.sph, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSph));
-        stage16(smem + a.lds_cc, a.sph_cc, a.lds_bodies - a.lds_cc);
+        stage16(smem + a.lds_cc, a.sph_cc, a.lds_pln - a.lds_cc);
+        stage16(smem + a.lds_pln, a.pln, (uint32_t)a.n_pln * (uint32_t)sizeof(RgPln));
+        stage16(smem + a.lds_dsk, a.dsk, (uint32_t)a.n_dsk * (uint32_t)sizeof(RgDsk));
+        stage16(smem + a.lds_box, a.box, a.lds_bodies - a.lds_box);
         src.f = reinterpret_cast<const RgSphF *>(smem);
         src.f2 = reinterpret_cast<const RgSphF2 *>(smem + (size_t)a.n_sph * sizeof(RgSphF));
         src.s = reinterpret_cast<const RgSph *>(smem + a.lds_sph);
         src.cc = reinterpret_cast<const double *>(smem + a.lds_cc);
+        src.pl = reinterpret_cast<const RgPln *>(smem + a.lds_pln);
+        src.dk = reinterpret_cast<const RgDsk *>(smem + a.lds_dsk);
+        src.bx = reinterpret_cast<const RgBox *>(smem + a.lds_box);
     } else {
         src.s = rg_cptr(a.sph);
         src.cc = rg_cptr(a.sph_cc);
         src.f = rg_cptr(a.sphf);
         src.f2 = rg_cptr(a.sphf2);
+        src.pl = rg_cptr(a.pln);
+        src.dk = rg_cptr(a.dsk);
+        src.bx = rg_cptr(a.box);
     }
     if constexpr (LCOLD) {
         stage16(smem + a.lds_bodies, a.bodies, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgBodyDev));
@@ -1085,7 +1101,8 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
     closest_init(c);
     bool occl = false;
     if (alive) {
-        SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc), rg_cptr(a.sphf), rg_cptr(a.sphf2)};
+        SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc), rg_cptr(a.sphf), rg_cptr(a.sphf2),
+                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box)};
         if (a.path == RG_PATH_HEAVY) trace_query<true>(a, src, r, false, 0.0, c, occl);
         else trace_query<false>(a, src, r, false, 0.0, c, occl);
         if (c.nan && c.nhit >= 2) raise_error(a, i, RG_ERR_NAN_DISTANCE);
@@ -1129,6 +1146,9 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
 #ifndef RG_LDS_BUDGET
 #define RG_LDS_BUDGET (160 * 1024)       // one block per CU owns the CU's LDS
 #endif
+#ifndef RG_HEAVY_WPS
+#define RG_HEAVY_WPS 4            // heavy path: waves per SIMD (block = 256 * WPS threads)
+#endif
 #ifndef RG_HEAVY_F32_FILTER
 #define RG_HEAVY_F32_FILTER true  // heavy path: f32 pre-filter in front of the exact sphere tests
 #endif
@@ -1153,10 +1173,11 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
     // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
     bool heavy = a->n_sph + a->n_pln + a->n_dsk + a->n_box >= RG_HEAVY_SCENE_BODIES;
 #if defined(RG_FORCE_WPS)
-    heavy = RG_FORCE_WPS == 4;
+    heavy = RG_FORCE_WPS != 2;
 #endif
     if (a->path != RG_PATH_AUTO) heavy = a->path == RG_PATH_HEAVY;
-    return heavy ? launch_waves<MAXD, 4, 1, RG_HEAVY_F32_FILTER>(a, stream) : launch_waves<MAXD, 2, RG_LB, false>(a, stream);
+    return heavy ? launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER>(a, stream)
+                 : launch_waves<MAXD, 2, RG_LB, false>(a, stream);
 }
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {
