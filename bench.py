@@ -206,6 +206,15 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt[0])
+    verified = None
+    if getattr(args, "verify", False):
+        final = rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
+        if rank == 0:
+            torch.cuda.synchronize(dev)
+            ref = ds.render_image(W, H)
+            verified = bool((final.cpu().numpy() == ref).all())
+            if not verified:
+                raise SystemExit(f"--verify: the {world}-rank frame differs from the 1-rank render")
     ds.close()
     if rank != 0:
         return None
@@ -249,6 +258,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
             "basis": f"{alg_bytes} B framebuffer written per launch (+{tex} B of textures, L2/MALL resident)",
         },
     }
+    if verified is not None:
+        res["verified_against_1_rank_frame"] = verified
     if cpu:
         res["cpu_baseline"] = cpu_baseline(scene, W, H)
         res["gpu_over_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
@@ -266,6 +277,11 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-north-star", action="store_true",
                     help="skip the extra north_star line item (1024 spheres, 3840x2160, depth 5)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo: rehearsal)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal: every rank renders on GPU 0 (use with --backend gloo)")
+    ap.add_argument("--verify", action="store_true",
+                    help="rank 0 checks the gathered frame against a 1-rank render, byte for byte")
     args = ap.parse_args()
 
     import torch
@@ -274,9 +290,14 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:
+        local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local_rank)

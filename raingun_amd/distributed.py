@@ -74,6 +74,19 @@ def render_frame(render_tiles: Callable[[object], object], height: int, rank: in
         return part[:height]
     import torch.distributed as dist
 
+    if part.is_cuda and dist.get_backend(group) == "gloo":
+        # rehearsal only (gloo gathers host tensors): stage through host memory
+        host = part.cpu()
+        if rank == 0:
+            hb = [host.new_empty(host.shape) for _ in range(world)]
+            dist.gather(host, hb, dst=0, group=group)
+            frame = assemble(hb, height, world, tile_rows).to(part.device)
+            if out is not None:
+                out.copy_(frame)
+                return out
+            return frame
+        dist.gather(host, None, dst=0, group=group)
+        return None
     if rank == 0:
         bufs = gather_bufs if gather_bufs is not None else [part.new_empty(part.shape) for _ in range(world)]
         dist.gather(part, bufs, dst=0, group=group)
