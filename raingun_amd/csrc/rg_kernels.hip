@@ -224,6 +224,9 @@ __device__ __forceinline__ bool filter_primary(const RgSphF &f, const RgSphF2 &f
     return !(opp > f2.thrp);
 }
 
+#ifndef RG_SPHERE_UV_NOINLINE
+#define RG_SPHERE_UV_NOINLINE 1
+#endif
 #ifndef RG_SPH_GROUP
 #define RG_SPH_GROUP 2     // spheres per exact miss-test group (one divergent branch per group)
 #endif
@@ -591,6 +594,19 @@ __device__ __forceinline__ bool surface_normal(const RgBodyDev &b, V3 h, V3 &n) 
     return true;
 }
 
+// Sphere texture coordinates (bodies.rs:126-132).  Kept out of line: the
+// f64 atan2/acos expansions need ~70 VGPRs, and inlined into the megakernel
+// they set its register peak (247 VGPRs) while every other live value waits.
+#if RG_SPHERE_UV_NOINLINE
+__device__ __attribute__((noinline))
+#else
+__device__ __forceinline__
+#endif
+void sphere_uv(double hx, double hy, double hz, double r, float &tx, float &ty) {
+    tx = (1.0f + ((float)atan2(hz, hx)) / PI_F) * 0.5f;
+    ty = ((float)acos(hy / r)) / PI_F;
+}
+
 // bodies.rs:126-132, 155-169, 198-212, 330-333
 __device__ __forceinline__ void texture_coords(const RgBodyDev &b, V3 h, float &tx, float &ty) {
     if (b.kind == RG_BODY_SPHERE) {
@@ -598,8 +614,7 @@ __device__ __forceinline__ void texture_coords(const RgBodyDev &b, V3 h, float &
 #ifdef RG_DBG_NO_ATAN  // timing ablation only (wrong images)
         tx = (float)hv.x; ty = (float)hv.y; return;
 #endif
-        tx = (1.0f + ((float)atan2(hv.z, hv.x)) / PI_F) * 0.5f;
-        ty = ((float)acos(hv.y / b.p[3])) / PI_F;
+        sphere_uv(hv.x, hv.y, hv.z, b.p[3], tx, ty);
     } else if (b.kind == RG_BODY_AABB) {
         tx = 0.0f;
         ty = 0.0f;
@@ -632,6 +647,17 @@ __device__ __forceinline__ C3 material_color(const RgTexDev *texs, const RgMatDe
     uint32_t px = t.texels[(size_t)y * (uint32_t)t.w + x];
     return c3((float)(px & 0xffu) / 255.0f, (float)((px >> 8) & 0xffu) / 255.0f,
               (float)((px >> 16) & 0xffu) / 255.0f);
+}
+
+// body.color(&body.texture_coords(hit)) (rendering.rs:134-135, 103).  The
+// texture coordinates are pure functions of the hit and only a Texture
+// coloration reads them, so they are computed for textured materials only:
+// a Color material yields the same colour without the atan2/acos/cross work.
+__device__ __forceinline__ C3 surface_color(const RgTexDev *texs, const RgMatDev &m, const RgBodyDev &b, V3 h) {
+    if (m.coloration == RG_COLORATION_COLOR) return c3(m.color[0], m.color[1], m.color[2]);
+    float tx, ty;
+    texture_coords(b, h, tx, ty);
+    return material_color(texs, m, tx, ty);
 }
 
 // rendering.rs:174-200, `cos_i = cos_t.abs()` (:194) kept as written.
@@ -904,17 +930,13 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                         V3 n;
                         if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
                         if (m.surface != RG_SURFACE_REFRACTIVE) {
-                            float tx, ty;
-                            texture_coords(b, h, tx, ty);
-                            bcol = material_color(T.texs, m, tx, ty);
+                            bcol = surface_color(T.texs, m, b, h);
                             fin = c3(0.0f, 0.0f, 0.0f);
                             hp = h; hn = n; hd = q.d; hb = c.id; hdepth = qdepth; li = 0;
                             shade = true;
                         } else {
                             float kr = (float)fresnel(q.d, n, m.index);
-                            float tx, ty;
-                            texture_coords(b, h, tx, ty);
-                            C3 surf = material_color(T.texs, m, tx, ty);
+                            C3 surf = surface_color(T.texs, m, b, h);
                             Ray rr = reflection(n, q.d, h);
                             int cd = qdepth + 1;
                             C3 tc = def;
@@ -1165,6 +1187,10 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream) {
     return launch_one<MAXD, false, false, WPS, LB, F32F>(a, 0, stream);
 }
 
+#ifndef RG_LIGHT_WPS
+#define RG_LIGHT_WPS 3            // light path: waves per SIMD (168 VGPRs)
+#endif
+
 template <int MAXD>
 static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
     // Light scenes (few bodies): per-iteration overhead dominates -> fewer,
@@ -1177,7 +1203,7 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
 #endif
     if (a->path != RG_PATH_AUTO) heavy = a->path == RG_PATH_HEAVY;
     return heavy ? launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER>(a, stream)
-                 : launch_waves<MAXD, 2, RG_LB, false>(a, stream);
+                 : launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false>(a, stream);
 }
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {
