@@ -31,7 +31,7 @@ constexpr double SHADOW_BIAS = 1e-13;                 // lib.rs:11
 constexpr float PI_F = 3.14159265358979323846f;       // std::f32::consts::PI
 
 enum : int { MODE_CLOSEST = 0, MODE_SHADOW = 1, MODE_DONE = 2 };
-enum : int { FR_REFL = 0, FR_REFR_T = 1, FR_REFR_R = 2 };
+enum : int { FR_REFL = 0, FR_REFR_T = 1, FR_REFR_R = 2, FR_REFL_PEND = 3 };
 
 struct V3 { double x, y, z; };
 struct C3 { float r, g, b; };
@@ -889,6 +889,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         Ray q;                 // current query (shadow: q.o = shared origin)
         ShadowBatch<LB> sb;        // shadow: the batch's directions and light distances
         uint32_t occl_full = 0u;
+        float pp[LB], lin[LB], refl_f = 0.0f;  // light path: per-light max(n.l, 0), intensity; albedo/pi
         int qdepth = 0;        // closest: depth of the ray
         // hit being shaded
         V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0), hd = v3(0, 0, 0);
@@ -931,9 +932,46 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                         if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
                         if (m.surface != RG_SURFACE_REFRACTIVE) {
                             bcol = surface_color(T.texs, m, b, h);
-                            fin = c3(0.0f, 0.0f, 0.0f);
-                            hp = h; hn = n; hd = q.d; hb = c.id; hdepth = qdepth; li = 0;
-                            shade = true;
+                            hb = c.id; hdepth = qdepth;
+                            if constexpr (LB > 1) {
+                                // ONE batch covers every light (n_lights <= LB on this path): set it
+                                // up now, with the per-light shading factors, so that no hit-point
+                                // state (h, n, incident) has to survive the shadow pass
+                                refl_f = m.albedo / PI_F;                               // rendering.rs:164
+                                if (m.surface == RG_SURFACE_REFLECTING && qdepth + 1 < max_depth) {
+                                    Frame &f = stk[sp++];                               // reflection ray of
+                                    const Ray rr = reflection(n, q.d, h);               // rendering.rs:88,
+                                    f.type = FR_REFL_PEND;                              // D filled in later
+                                    f.rr[0] = rr.o.x; f.rr[1] = rr.o.y; f.rr[2] = rr.o.z;
+                                    f.rr[3] = rr.d.x; f.rr[4] = rr.d.y; f.rr[5] = rr.d.z;
+                                    f.f[3] = m.reflectivity;
+                                    f.cdepth = qdepth + 1;
+                                }
+                                q.o = add(h, scl(n, SHADOW_BIAS));                      // rendering.rs:148
+                                occl_full = 0u;
+#pragma unroll
+                                for (int l = 0; l < LB; ++l) {
+                                    if (l < a.n_lights) {
+                                        const RgLightDev L = T.lights[l];
+                                        light_dir_dist(L, h, sb.d[l], sb.ld[l]);
+                                        pp[l] = fmaxf((float)dot(n, sb.d[l]), 0.0f);    // rendering.rs:161-162
+                                        lin[l] = light_intensity(L, h);                 // pure; used if lit
+                                        occl_full |= 1u << l;
+                                        n_shadow++;
+                                    } else {
+                                        sb.d[l] = v3(0.0, 0.0, 1.0);
+                                        sb.ld[l] = 0.0;
+                                        pp[l] = 0.0f;
+                                        lin[l] = 0.0f;
+                                    }
+                                }
+                                if (a.n_lights > 0) mode = MODE_SHADOW;
+                                else shade = true;  // no lights: finish with black (rendering.rs:138)
+                            } else {
+                                fin = c3(0.0f, 0.0f, 0.0f);
+                                hp = h; hn = n; hd = q.d; li = 0;
+                                shade = true;
+                            }
                         } else {
                             float kr = (float)fresnel(q.d, n, m.index);
                             C3 surf = surface_color(T.texs, m, b, h);
@@ -974,8 +1012,45 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                 } else {
                     shade = true;  // a shadow result for light li
                 }
-                if (shade) {
-                    // shade_diffuse loop body (rendering.rs:141-170), LB lights per batch
+                if constexpr (LB > 1) {
+                  if (shade) {
+                    // shade_diffuse accumulation over the batch (rendering.rs:141-170), in light order
+                    const RgMatDev m = T.mats[hb];
+                    C3 acc = c3(0.0f, 0.0f, 0.0f);
+#pragma unroll
+                    for (int l = 0; l < LB; ++l) {
+                        if (l < a.n_lights) {
+                            const RgLightDev L = T.lights[l];
+                            const float inten = !((occl >> l) & 1u) ? lin[l] : 0.0f;
+                            const float power = pp[l] * inten;
+                            C3 lc = cscl(cscl(c3(L.color[0], L.color[1], L.color[2]), power), refl_f);
+                            acc = cadd(acc, cmul(bcol, lc));
+                        }
+                    }
+                    C3 dcol = cclamp(acc);
+                    if (m.surface == RG_SURFACE_DIFFUSE) {
+                        ret = dcol;
+                        unwind = true;
+                    } else {  // Reflecting (rendering.rs:86-91)
+                        const float r = m.reflectivity;
+                        const int cd = hdepth + 1;
+                        if (cd >= max_depth) {
+                            ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
+                            unwind = true;
+                        } else {
+                            Frame &f = stk[sp - 1];  // the FR_REFL_PEND pushed at the hit
+                            f.type = FR_REFL;
+                            f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b;
+                            q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
+                            q.d = v3(f.rr[3], f.rr[4], f.rr[5]);
+                            qdepth = cd;
+                            mode = MODE_CLOSEST;
+                            n_sec++;
+                        }
+                    }
+                  }
+                } else if (shade) {
+                    // shade_diffuse loop body (rendering.rs:141-170), one light per iteration
                     const RgMatDev m = T.mats[hb];
                     if (rmode == MODE_SHADOW) {
                         const float refl = m.albedo / PI_F;
@@ -1202,6 +1277,7 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
     heavy = RG_FORCE_WPS != 2;
 #endif
     if (a->path != RG_PATH_AUTO) heavy = a->path == RG_PATH_HEAVY;
+    if (a->n_lights > RG_LB) heavy = true;  // the light path shades all lights in ONE batch
     return heavy ? launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER>(a, stream)
                  : launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false>(a, stream);
 }
