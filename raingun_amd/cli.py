@@ -7,18 +7,16 @@ Flags and their precedence follow construct_app / RenderOptions::from
 (main.rs:74-75, 119-123); --hd / --4k set 1920x1080 / 3840x2160 and override
 each other (the last one wins); explicit --width/--height override presets
 (but not --draft, which clap treats as overriding them, main.rs:47-54).  The
-render itself runs on the GPU (rg_render_image); the PNG is written by a
-self-contained encoder (zlib), and the timing line matches
+render itself runs on the GPU (rg_render_image); the scene is loaded and the
+PNG written by the native host layer (libraingun_host.so), and the timing line matches
 print_render_message (render.rs:218-244).  `--preview` (piston window) is not
 supported: there is no display on an MI355X node.
 """
 from __future__ import annotations
 
 import argparse
-import struct
 import sys
 import time
-import zlib
 from dataclasses import dataclass
 from pathlib import Path
 from typing import List, Optional
@@ -94,19 +92,10 @@ def parse_arguments(args: List[str]) -> RenderOptions:
 
 # ---------------------------------------------------------------- PNG (RGBA8)
 def encode_png(rgba: np.ndarray) -> bytes:
-    """Minimal PNG encoder: 8-bit RGBA, filter 0 on every row, zlib level 6."""
-    rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
-    h, w, c = rgba.shape
-    assert c == 4
+    """8-bit RGBA PNG through the native encoder (rgh_png_encode, render.rs:58)."""
+    from . import _host
 
-    def chunk(tag: bytes, data: bytes) -> bytes:
-        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
-
-    raw = np.zeros((h, 1 + 4 * w), dtype=np.uint8)
-    raw[:, 1:] = rgba.reshape(h, 4 * w)
-    ihdr = struct.pack(">IIBBBBB", w, h, 8, 6, 0, 0, 0)
-    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", zlib.compress(raw.tobytes(), 6)) +
-            chunk(b"IEND", b""))
+    return _host.encode_png(rgba)
 
 
 def format_duration(ms: int) -> str:  # render.rs:229-244

@@ -1,14 +1,17 @@
 """Host-side mirror of raingun-lib's public API (scene.rs, bodies.rs, lights.rs,
 material.rs) above the C ABI of libraingun_hip.so.
 
-* :func:`load_scene` reproduces the serde schema of `Scene` (scene.rs:11-31)
-  as serde_yaml 0.6 reads it: camelCase top-level keys with
+* :func:`load_scene` runs the native C++ loader (include/raingun_host.h), which
+  reproduces the serde schema of `Scene` (scene.rs:11-31) as serde_yaml 0.6
+  over yaml-rust 0.3.5 reads it: camelCase top-level keys with
   `deny_unknown_fields`; externally tagged enums (`Sphere:`/`Plane:`/`Disk:`/
   `AABB:`, `Directional:`/`Spherical:`, `Color:`/`Texture:`, `Diffuse` /
   `{Diffuse: null}` / `{Reflecting: {...}}` / `{Refractive: {...}}`); Point3 and
   Vector3 as `[x, y, z]` or `{x:, y:, z:}` (cgmath "eders"); f32 fields rounded
   to f32; textures decoded eagerly at load time relative to the working
-  directory (material.rs:34-47).
+  directory (material.rs:34-47) by the native decoder (libraingun_host.so),
+  which rounds like the reference's jpeg-decoder 0.1.11.  This module only
+  converts the loaded rg_scene_desc into the dataclasses below.
 * :class:`Scene` keeps the reference's `render_image(width, height)` /
   `streaming_render(...)` / `trace(ray)` entry points (scene.rs:34-51); every
   one of them runs on the GPU through the C ABI.  There is no CPU fallback.
@@ -16,7 +19,6 @@ material.rs) above the C ABI of libraingun_hip.so.
 from __future__ import annotations
 
 import ctypes as C
-import math
 import os
 from dataclasses import dataclass, field
 from pathlib import Path
@@ -27,7 +29,6 @@ import numpy as np
 from . import _abi
 from .color import Color
 
-F32 = np.float32
 
 
 class SceneError(ValueError):
@@ -99,192 +100,67 @@ Body = Union[Sphere, Plane, Disk, AABB]
 Light = Union[DirectionalLight, SphericalLight]
 
 
-# ---------------------------------------------------------------- YAML schema
-def _f64(v, what: str) -> float:
-    if isinstance(v, bool) or v is None:
-        raise SceneError(f"{what}: expected a number, got {v!r}")
-    if isinstance(v, (int, float)):
-        return float(v)
-    if isinstance(v, str):  # PyYAML (YAML 1.1) leaves e.g. "1e-13" as a string; yaml-rust parses it
-        try:
-            return float(v.strip())
-        except ValueError:
-            pass
-    raise SceneError(f"{what}: expected a number, got {v!r}")
-
-
-def _f32(v, what: str) -> float:
-    return float(F32(_f64(v, what)))
-
-
-def _u32(v, what: str) -> int:
-    if isinstance(v, bool) or not isinstance(v, int) or v < 0 or v > 0xFFFFFFFF:
-        raise SceneError(f"{what}: expected a u32, got {v!r}")
-    return int(v)
-
-
-def _vec3(v, what: str) -> tuple:
-    if isinstance(v, (list, tuple)):
-        if len(v) != 3:
-            raise SceneError(f"{what}: expected 3 components, got {len(v)}")
-        return tuple(_f64(c, what) for c in v)
-    if isinstance(v, dict):
-        try:
-            return (_f64(v["x"], what), _f64(v["y"], what), _f64(v["z"], what))
-        except KeyError as e:
-            raise SceneError(f"{what}: missing field {e.args[0]}") from None
-    raise SceneError(f"{what}: expected a point/vector, got {v!r}")
-
-
-def _color(v, what: str) -> Color:
-    if not isinstance(v, str):
-        raise SceneError(f"{what}: a string of a simple hex color (#000000 - #ffffff), got {v!r}")
-    try:
-        return Color.from_str(v)
-    except ValueError as e:
-        raise SceneError(f"{what}: {e}") from None
-
-
-def _variant(v, what: str):
-    """Externally tagged enum: 'Name' (unit variant) or {Name: content}."""
-    if isinstance(v, str):
-        return v, None
-    if isinstance(v, dict) and len(v) == 1:
-        (k, val), = v.items()
-        return k, val
-    raise SceneError(f"{what}: expected an enum variant, got {v!r}")
-
-
-def _req(d, key: str, what: str):
-    if not isinstance(d, dict):
-        raise SceneError(f"{what}: expected a mapping, got {d!r}")
-    if key not in d:
-        raise SceneError(f"{what}: missing field `{key}`")
-    return d[key]
-
-
-def _load_image(path: str, base: Path) -> np.ndarray:
-    p = Path(path)
-    if not p.is_absolute():
-        p = base / p
-    try:
-        from PIL import Image  # decoder used by the host loader only (image::open, material.rs:42)
-        with Image.open(p) as im:
-            return np.ascontiguousarray(np.asarray(im.convert("RGBA"), dtype=np.uint8))
-    except Exception as e:  # serde Error::custom (material.rs:43-46)
-        raise SceneError(f"Could not load texture file {path}: {e}") from None
-
-
-def _material(v, what: str, base: Path, cache: dict) -> Material:
-    kind, col = _variant(_req(v, "coloration", what), what + ".coloration")
-    if kind == "Color":
-        coloration = _color(col, what + ".coloration.Color")
-    elif kind == "Texture":
-        tw = what + ".coloration.Texture"
-        img_path = _req(col, "image", tw)
-        if not isinstance(img_path, str):
-            raise SceneError(f"{tw}.image: expected a path string")
-        if img_path not in cache:
-            cache[img_path] = _load_image(img_path, base)
-        coloration = Texture(img_path, cache[img_path], _f32(_req(col, "x_offset", tw), tw + ".x_offset"),
-                             _f32(_req(col, "y_offset", tw), tw + ".y_offset"))
-    else:
-        raise SceneError(f"{what}.coloration: unknown variant `{kind}`, expected `Color` or `Texture`")
-    albedo = _f32(_req(v, "albedo", what), what + ".albedo")
-    skind, sval = _variant(_req(v, "surface", what), what + ".surface")
-    m = Material(coloration, albedo, skind)
-    if skind == "Diffuse":
-        if sval is not None:
-            raise SceneError(f"{what}.surface: Diffuse takes no fields")
-    elif skind == "Reflecting":
-        m.reflectivity = _f32(_req(sval, "reflectivity", what + ".surface"), what + ".reflectivity")
-    elif skind == "Refractive":
-        m.index = _f32(_req(sval, "index", what + ".surface"), what + ".index")
-        m.transparency = _f32(_req(sval, "transparency", what + ".surface"), what + ".transparency")
-    else:
-        raise SceneError(f"{what}.surface: unknown variant `{skind}`")
-    return m
-
-
-def _body(v, i: int, base: Path, cache: dict) -> Body:
-    what = f"bodies[{i}]"
-    kind, b = _variant(v, what)
-    w = f"{what}.{kind}"
-    if kind == "Sphere":
-        return Sphere(_vec3(_req(b, "center", w), w + ".center"), _f64(_req(b, "radius", w), w + ".radius"),
-                      _material(_req(b, "material", w), w + ".material", base, cache))
-    if kind == "Plane":
-        return Plane(_vec3(_req(b, "origin", w), w + ".origin"), _vec3(_req(b, "normal", w), w + ".normal"),
-                     _material(_req(b, "material", w), w + ".material", base, cache))
-    if kind == "Disk":
-        return Disk(_vec3(_req(b, "origin", w), w + ".origin"), _vec3(_req(b, "normal", w), w + ".normal"),
-                    _f64(_req(b, "radius", w), w + ".radius"),
-                    _material(_req(b, "material", w), w + ".material", base, cache))
-    if kind == "AABB":
-        bounds = _req(b, "bounds", w)
-        if not isinstance(bounds, (list, tuple)) or len(bounds) != 2:
-            raise SceneError(f"{w}.bounds: expected two points")
-        return AABB((_vec3(bounds[0], w + ".bounds[0]"), _vec3(bounds[1], w + ".bounds[1]")),
-                    _material(_req(b, "material", w), w + ".material", base, cache))
-    raise SceneError(f"{what}: unknown variant `{kind}`, expected one of `Sphere`, `Plane`, `Disk`, `AABB`")
-
-
-def _light(v, i: int) -> Light:
-    what = f"lights[{i}]"
-    kind, l = _variant(v, what)
-    w = f"{what}.{kind}"
-    if kind == "Directional":
-        return DirectionalLight(_vec3(_req(l, "direction", w), w + ".direction"),
-                                _color(_req(l, "color", w), w + ".color"),
-                                _f32(_req(l, "intensity", w), w + ".intensity"))
-    if kind == "Spherical":
-        return SphericalLight(_vec3(_req(l, "position", w), w + ".position"),
-                              _color(_req(l, "color", w), w + ".color"),
-                              _f32(_req(l, "intensity", w), w + ".intensity"))
-    raise SceneError(f"{what}: unknown variant `{kind}`, expected `Directional` or `Spherical`")
-
-
-_SCENE_KEYS = ("fov", "defaultColor", "maxRecursionDepth", "bodies", "lights")
-
-
+# ---------------------------------------------------------------- loading
 def load_scene(source: Union[str, os.PathLike], texture_root: Optional[Union[str, os.PathLike]] = None) -> "Scene":
-    """serde_yaml::from_reader::<Scene> (main.rs:116-118).  `source` is a path or
-    YAML text.  Texture paths resolve against `texture_root` (default: the
-    current working directory, as image::open does)."""
-    import yaml
+    """serde_yaml::from_reader::<Scene> (main.rs:116-118) through the native
+    loader (rgh_scene_load_*, raingun_amd/host/scene_loader.cpp).  `source` is
+    a path or YAML text.  Texture paths resolve against `texture_root`
+    (default: the current working directory, as image::open does)."""
+    from . import _host
 
-    text = None
-    if isinstance(source, os.PathLike) or (isinstance(source, str) and "\n" not in source and Path(source).exists()):
-        text = Path(source).read_text()
-    else:
-        text = str(source)
     try:
-        doc = yaml.safe_load(text)
-    except yaml.YAMLError as e:
-        raise SceneError(f"Could not load YAML: {e}") from None
-    if doc is None:
-        doc = {}
-    if not isinstance(doc, dict):
-        raise SceneError("invalid type: expected struct Scene")
-    for k in doc:
-        if k not in _SCENE_KEYS:  # deny_unknown_fields (scene.rs:12)
-            raise SceneError(f"unknown field `{k}`, expected one of {', '.join('`%s`' % s for s in _SCENE_KEYS)}")
-    base = Path(texture_root) if texture_root is not None else Path.cwd()
-    cache: dict = {}
-    s = Scene()
-    if "fov" in doc:
-        s.fov = _f64(doc["fov"], "fov")
-    if "defaultColor" in doc:
-        s.default_color = _color(doc["defaultColor"], "defaultColor")
-    if "maxRecursionDepth" in doc:
-        s.max_recursion_depth = _u32(doc["maxRecursionDepth"], "maxRecursionDepth")
-    bodies = doc.get("bodies", []) or []
-    lights = doc.get("lights", []) or []
-    if not isinstance(bodies, list) or not isinstance(lights, list):
-        raise SceneError("bodies/lights: expected a sequence")
-    s.bodies = [_body(b, i, base, cache) for i, b in enumerate(bodies)]
-    s.lights = [_light(l, i) for i, l in enumerate(lights)]
-    return s
+        if isinstance(source, os.PathLike) or (isinstance(source, str) and "\n" not in source
+                                               and Path(source).exists()):
+            loaded = _host.LoadedScene.from_file(source, texture_root)
+        else:
+            loaded = _host.LoadedScene.from_string(str(source), texture_root)
+    except _host.HostError as e:
+        raise SceneError(str(e)) from None
+    try:
+        return _scene_from_desc(loaded)
+    finally:
+        loaded.close()
+
+
+_SURFACES = {_abi.SURFACE_DIFFUSE: "Diffuse", _abi.SURFACE_REFLECTING: "Reflecting",
+             _abi.SURFACE_REFRACTIVE: "Refractive"}
+
+
+def _scene_from_desc(loaded) -> "Scene":
+    d = loaded.desc
+    textures = []
+    for i in range(d.n_textures):
+        t = d.textures[i]
+        img = np.ctypeslib.as_array(t.rgba, shape=(t.height * t.width * 4,)).copy().reshape(t.height, t.width, 4)
+        textures.append((loaded.texture_path(i), img))
+
+    def material(m) -> Material:
+        if m.coloration == _abi.COLORATION_TEXTURE:
+            path, img = textures[m.texture]
+            col: Union[Color, Texture] = Texture(path, img, m.x_offset, m.y_offset)
+        else:
+            col = Color(*m.color)
+        return Material(col, m.albedo, _SURFACES[m.surface], m.reflectivity, m.index, m.transparency)
+
+    bodies: List[Body] = []
+    for i in range(d.n_bodies):
+        b = d.bodies[i]
+        p = tuple(b.p)
+        mat = material(b.material)
+        if b.kind == _abi.BODY_SPHERE:
+            bodies.append(Sphere(p[0:3], p[3], mat))
+        elif b.kind == _abi.BODY_PLANE:
+            bodies.append(Plane(p[0:3], p[3:6], mat))
+        elif b.kind == _abi.BODY_DISK:
+            bodies.append(Disk(p[0:3], p[3:6], p[6], mat))
+        else:
+            bodies.append(AABB((p[0:3], p[3:6]), mat))
+    lights: List[Light] = []
+    for i in range(d.n_lights):
+        l = d.lights[i]
+        cls = DirectionalLight if l.kind == _abi.LIGHT_DIRECTIONAL else SphericalLight
+        lights.append(cls(tuple(l.v), Color(*l.color), l.intensity))
+    return Scene(d.fov, Color(*d.default_color), d.max_recursion_depth, bodies, lights)
 
 
 # ---------------------------------------------------------------- flat descriptor

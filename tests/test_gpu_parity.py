@@ -52,6 +52,20 @@ def test_examples_800x600(oracle_lib, example_scenes, name, path):
     assert st.rays.primary == 800 * 600
 
 
+@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("name", ["test1", "test2", "test3"])
+def test_examples_reproduce_reference_golden_png(example_scenes, golden_dir, name, path):
+    """The GPU output equals the reference's own renders byte for byte
+    (examples/test{1,2,3}.png, 800x600, YAML depth), textures included."""
+    from PIL import Image
+
+    ds = DeviceScene(example_scenes[name], path=path)
+    got = ds.render_image(800, 600)
+    ds.close()
+    gold = np.asarray(Image.open(golden_dir / "examples" / f"{name}.png").convert("RGBA"))
+    assert np.array_equal(got, gold)
+
+
 def test_config2_test1_4k_depth5(oracle_lib, example_scenes):
     s = copy.copy(example_scenes["test1"])
     s.max_recursion_depth = 5
