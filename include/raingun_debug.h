@@ -17,6 +17,22 @@ extern "C" {
  * 1 = heavy path (4 waves/SIMD, one ray per lane, f32 pre-filter + exact f64). */
 rg_status rg_debug_set_path(rg_scene *scene, int32_t path);
 
+/* Sphere BVH (built by rg_scene_create for scenes with at
+ * least 16 spheres and used by the heavy path and rg_trace).  Disabling it
+ * makes every ray scan all spheres; results are identical either way. */
+typedef struct rg_bvh_info {
+    int32_t built;         /* a BVH exists for this scene */
+    int32_t enabled;       /* and is used by the render/trace launches */
+    int32_t nodes;         /* 4-wide nodes (128 B each) */
+    int32_t leaves;        /* leaves (<= 4 spheres each) */
+    int32_t depth;         /* levels */
+    float margin;          /* box inflation, scene units */
+    float origin_bound;    /* rays with |o_k| above this scan all spheres */
+    int32_t _pad;
+} rg_bvh_info;
+rg_status rg_debug_set_bvh(rg_scene *scene, int32_t enable);
+rg_status rg_debug_bvh_info(const rg_scene *scene, rg_bvh_info *info);
+
 #ifdef __cplusplus
 }
 #endif

@@ -107,6 +107,11 @@ class rg_tiling(C.Structure):
     _fields_ = [("tile_rows", C.c_uint32), ("tile_stride", C.c_uint32), ("tile_offset", C.c_uint32)]
 
 
+class rg_bvh_info(C.Structure):  # include/raingun_debug.h
+    _fields_ = [("built", C.c_int32), ("enabled", C.c_int32), ("nodes", C.c_int32), ("leaves", C.c_int32),
+                ("depth", C.c_int32), ("margin", C.c_float), ("origin_bound", C.c_float), ("_pad", C.c_int32)]
+
+
 TILE_CALLBACK = C.CFUNCTYPE(C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8), C.c_void_p)
 
 # Every symbol include/raingun.h declares (tests/test_abi.py checks the export table).
@@ -125,7 +130,7 @@ EXPORTED_SYMBOLS = (
     "rg_trace",
 )
 # include/raingun_debug.h
-DEBUG_SYMBOLS = ("rg_debug_set_path",)
+DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info")
 PATH_AUTO, PATH_LIGHT, PATH_HEAVY = -1, 0, 1
 
 
@@ -168,6 +173,10 @@ def _declare(lib: C.CDLL) -> None:
                                      P(rg_stats)]
     lib.rg_debug_set_path.restype = C.c_int32
     lib.rg_debug_set_path.argtypes = [C.c_void_p, C.c_int32]
+    lib.rg_debug_set_bvh.restype = C.c_int32
+    lib.rg_debug_set_bvh.argtypes = [C.c_void_p, C.c_int32]
+    lib.rg_debug_bvh_info.restype = C.c_int32
+    lib.rg_debug_bvh_info.argtypes = [C.c_void_p, P(rg_bvh_info)]
     lib.rg_trace.restype = C.c_int32
     lib.rg_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
 

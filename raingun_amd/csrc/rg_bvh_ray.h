@@ -1,0 +1,75 @@
+// rg_bvh_ray.h — the f32 ray/box slab test of the BVH traversal, shared by the
+// kernel (rg_kernels.hip) and the CPU simulation test (tests/native/bvh_sim.cpp)
+// so the host check exercises the very expressions the GPU runs.
+//
+// Conservativeness (rg_bvh.cpp header): for a ray with |o_k| <= bvh_obound and
+// ||d|^2 - 1| <= 1e-13, every child box containing a sphere the exact test can
+// accept at t <= tb passes child_hit().  Directions are clamped to
+// |d_k| >= 1e-20 so 1/d is finite (no inf*0 NaNs); for a relevant ray that
+// only widens the slab interval of a near-parallel axis.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "rg_device.h"
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RG_RCPF(x) __builtin_amdgcn_rcpf(x)  // v_rcp_f32: <= 1 ulp, covered by the margin
+#define RG_FMAF(a, b, c) __builtin_fmaf(a, b, c)
+#else
+#define RG_RCPF(x) (1.0f / (x))
+#define RG_FMAF(a, b, c) fmaf(a, b, c)
+#endif
+
+struct RayB {
+    float ix, iy, iz;     // 1 / d (f32)
+    float oix, oiy, oiz;  // o * (1 / d)
+};
+
+__device__ __forceinline__ float rg_bvh_clamp_dir(float v) {
+    const float lim = 1e-20f;
+    return fabsf(v) >= lim ? v : (v < 0.0f ? -lim : lim);
+}
+
+__device__ __forceinline__ RayB rg_make_rayb(double ox, double oy, double oz, double dx, double dy, double dz) {
+    RayB r;
+    r.ix = RG_RCPF(rg_bvh_clamp_dir((float)dx));
+    r.iy = RG_RCPF(rg_bvh_clamp_dir((float)dy));
+    r.iz = RG_RCPF(rg_bvh_clamp_dir((float)dz));
+    r.oix = (float)ox * r.ix;
+    r.oiy = (float)oy * r.iy;
+    r.oiz = (float)oz * r.iz;
+    return r;
+}
+
+// Smallest float >= t for t >= 0 (t = +inf stays inf).
+__device__ __forceinline__ float rg_f32_up(double t) {
+    float f = (float)t;
+    if ((double)f < t) {
+        uint32_t b;
+        memcpy(&b, &f, 4);
+        ++b;
+        memcpy(&f, &b, 4);
+    }
+    return f;
+}
+
+// Slab test of child k of N against [0, tb]; tn = entry distance (f32).
+__device__ __forceinline__ bool rg_child_hit(const RgBvhNode &N, int k, const RayB &r, float tb, float &tn) {
+    const float tx1 = RG_FMAF(N.lox[k], r.ix, -r.oix), tx2 = RG_FMAF(N.hix[k], r.ix, -r.oix);
+    const float ty1 = RG_FMAF(N.loy[k], r.iy, -r.oiy), ty2 = RG_FMAF(N.hiy[k], r.iy, -r.oiy);
+    const float tz1 = RG_FMAF(N.loz[k], r.iz, -r.oiz), tz2 = RG_FMAF(N.hiz[k], r.iz, -r.oiz);
+    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fmaxf(fminf(tz1, tz2), 0.0f));
+    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fminf(fmaxf(tz1, tz2), tb));
+    tn = tmin;
+    return tmin <= tmax;
+}
+
+// Rays the boxes are conservative for (NaN anywhere -> false).
+__device__ __forceinline__ bool rg_bvh_ray_ok(float obound, double ox, double oy, double oz, double dx, double dy,
+                                              double dz) {
+    const double dd = (dx * dx + dy * dy) + dz * dz;
+    const double ob = (double)obound;
+    return fabs(ox) <= ob && fabs(oy) <= ob && fabs(oz) <= ob && fabs(dd - 1.0) <= 1e-13;
+}

@@ -13,9 +13,14 @@
 
 #include "../../include/raingun.h"
 #include "../../include/raingun_debug.h"
+#include "rg_bvh.h"
 #include "rg_device.h"
 
 #pragma clang fp contract(off)
+
+#ifndef RG_BVH_MIN_SPHERES
+#define RG_BVH_MIN_SPHERES 16  // below this a scan of the sphere table is as cheap as a traversal
+#endif
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream);
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,
@@ -41,6 +46,11 @@ struct rg_scene {
     RgMatDev *mats = nullptr;
     RgLightDev *lights = nullptr;
     RgTexDev *texs = nullptr;
+    RgBvhNode *nodes = nullptr;  // sphere BVH (sphere tables are in its leaf order)
+    int32_t n_nodes = 0;
+    bool bvh_enabled = true;
+    float bvh_obound = 0.0f;
+    rg_bvh_info bvh_info{};
     unsigned long long *counters = nullptr;  // RG_COUNTER_WORDS words (rg_device.h)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
@@ -120,6 +130,10 @@ RgKernelArgs make_args(const rg_scene *s) {
     a.n_pln = s->n_pln;
     a.n_dsk = s->n_dsk;
     a.n_box = s->n_box;
+    const bool bvh = s->bvh_enabled && s->n_nodes > 0;
+    a.nodes = bvh ? s->nodes : nullptr;
+    a.n_nodes = bvh ? s->n_nodes : 0;
+    a.bvh_obound = s->bvh_obound;
     a.bodies = s->bodies;
     a.mats = s->mats;
     a.lights = s->lights;
@@ -127,11 +141,12 @@ RgKernelArgs make_args(const rg_scene *s) {
     a.n_bodies = s->n_bodies;
     a.n_lights = s->n_lights;
     a.n_textures = s->n_textures;
-    // LDS arena: [sphf | sphf2 | sph | cc (padded to 16 B) | pln | dsk | box (padded) | bodies | mats | lights | texs]
+    // LDS arena: [sphf | sphf2 | sph | cc (padded to 16 B) | nodes | pln | dsk | box (padded) | bodies | mats | lights | texs]
     auto al16 = [](uint32_t v) { return (v + 15u) & ~15u; };
     a.lds_sph = (uint32_t)s->n_sph * (uint32_t)(sizeof(RgSphF) + sizeof(RgSphF2));
     a.lds_cc = a.lds_sph + (uint32_t)s->n_sph * (uint32_t)sizeof(RgSph);
-    a.lds_pln = al16(a.lds_cc + (uint32_t)s->n_sph * 8u);
+    a.lds_nodes = al16(a.lds_cc + (uint32_t)s->n_sph * 8u);
+    a.lds_pln = a.lds_nodes + (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode);
     a.lds_dsk = a.lds_pln + (uint32_t)s->n_pln * (uint32_t)sizeof(RgPln);
     a.lds_box = a.lds_dsk + (uint32_t)s->n_dsk * (uint32_t)sizeof(RgDsk);
     a.lds_bodies = al16(a.lds_box + (uint32_t)s->n_box * (uint32_t)sizeof(RgBox));
@@ -222,6 +237,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
     if (!ok(hipSetDevice(device))) { release(s); return RG_ERR_DEVICE; }
 
     std::vector<RgSph> sph;
+    std::vector<double> sph_raw;  // center xyz, radius (BVH build input)
     std::vector<RgSphF> sphf;
     std::vector<RgSphF2> sphf2;
     std::vector<double> sph_cc;
@@ -259,6 +275,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
             make_filter_records(p, sphf.back(), sphf2.back());
             sph_cc.push_back(dot3(p, p));  // padded to an even count after the loop
             sph_id.push_back((int32_t)i);
+            sph_raw.insert(sph_raw.end(), p, p + 4);
             break;
         case RG_BODY_PLANE:
             pln.push_back(RgPln{p[0], p[1], p[2], p[3], p[4], p[5], dot3(p, p + 3), 0.0});
@@ -273,6 +290,27 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
             box_id.push_back((int32_t)i);
             break;
         }
+    }
+    // Sphere BVH: reorder the sphere tables into leaf order (sph_id keeps the
+    // YAML index, so the closest-hit tie-break is unaffected).
+    RgBvhBuild bvh;
+    if ((int)sph.size() >= RG_BVH_MIN_SPHERES && rg_build_bvh(sph_raw.data(), (int)sph.size(), bvh)) {
+        auto permute = [&](auto &v) {
+            auto old = v;
+            for (size_t j = 0; j < bvh.order.size(); ++j) v[j] = old[bvh.order[j]];
+        };
+        permute(sph);
+        permute(sphf);
+        permute(sphf2);
+        permute(sph_cc);
+        permute(sph_id);
+        s->bvh_obound = bvh.obound;
+        s->bvh_info.built = 1;
+        s->bvh_info.nodes = (int32_t)bvh.nodes.size();
+        s->bvh_info.leaves = bvh.leaves;
+        s->bvh_info.depth = bvh.depth;
+        s->bvh_info.margin = (float)bvh.margin;
+        s->bvh_info.origin_bound = bvh.obound;
     }
     if (sph_cc.size() % 2) sph_cc.push_back(0.0);  // LDS staging copies 16-B units
     std::vector<RgLightDev> lights(d->n_lights);
@@ -317,7 +355,9 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
     RG_UP(bodies, bodies);
     RG_UP(mats, mats);
     RG_UP(lights, lights);
+    RG_UP(nodes, bvh.nodes);
 #undef RG_UP
+    s->n_nodes = (int32_t)bvh.nodes.size();
     // textures: RGBA8 -> one u32 per texel (one 4-byte gather per lookup)
     std::vector<RgTexDev> texs(d->n_textures);
     for (uint32_t i = 0; st == RG_OK && i < d->n_textures; ++i) {
@@ -491,6 +531,19 @@ rg_status rg_render_stream(const rg_scene *s, uint32_t width, uint32_t height, u
 rg_status rg_debug_set_path(rg_scene *s, int32_t path) {
     if (!s || path < RG_PATH_AUTO || path > RG_PATH_HEAVY) return RG_ERR_INVALID_ARGUMENT;
     s->path = path;
+    return RG_OK;
+}
+
+rg_status rg_debug_set_bvh(rg_scene *s, int32_t enable) {
+    if (!s || (enable != 0 && enable != 1)) return RG_ERR_INVALID_ARGUMENT;
+    s->bvh_enabled = enable != 0;
+    return RG_OK;
+}
+
+rg_status rg_debug_bvh_info(const rg_scene *s, rg_bvh_info *info) {
+    if (!s || !info) return RG_ERR_INVALID_ARGUMENT;
+    *info = s->bvh_info;
+    info->enabled = s->bvh_enabled && s->n_nodes > 0;
     return RG_OK;
 }
 

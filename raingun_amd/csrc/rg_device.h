@@ -17,6 +17,11 @@
 #pragma once
 #include <stdint.h>
 
+#if !defined(__HIP__) && !defined(__HIPCC__)  // plain C++ (host-only builds and tests of rg_bvh.cpp)
+#define __device__
+#define __forceinline__ inline
+#endif
+
 // Hot tables are read through the constant address space (addrspace 4) in
 // device code: with a wave-uniform index that always lowers to s_load_* (SGPR
 // operands, scalar cache), never to per-lane vector loads.
@@ -36,6 +41,18 @@ struct alignas(16) RgSphF2 { float cchi, thrp, cc32, pad; };  // |c|^2 rounded u
 struct alignas(16) RgPln { double ox, oy, oz, nx, ny, nz, on, pad; };
 struct alignas(16) RgDsk { double ox, oy, oz, nx, ny, nz, r, on; };
 struct alignas(16) RgBox { double lo[3], hi[3]; };
+
+// 4-wide BVH over the sphere table (built on the host, rg_bvh.cpp).  Child
+// boxes are f32, inflated and rounded outward so that the f32 slab test can
+// only err towards "visit" (derivation: rg_kernels.hip, "BVH traversal").
+// child[k] >= 0: internal node; child[k] < 0: leaf, v = ~child[k], spheres
+// [v >> 3, (v >> 3) + (v & 7) + 1) of the (BVH-ordered) sphere tables.
+struct alignas(16) RgBvhNode {
+    float lox[4], loy[4], loz[4], hix[4], hiy[4], hiz[4];
+    int32_t child[4];
+    int32_t nchild;        // valid children (2..4)
+    int32_t pad[3];
+};
 
 struct RgBodyDev {         // per body, YAML order
     int32_t kind;
@@ -85,6 +102,10 @@ struct RgKernelArgs {
     const RgBox *box;
     const int32_t *box_id;
     int32_t n_sph, n_pln, n_dsk, n_box;
+    // BVH over the spheres (n_nodes == 0: none; brute-force sphere loops)
+    const RgBvhNode *nodes;
+    int32_t n_nodes;
+    float bvh_obound;        // rays with |o_k| > bvh_obound (or NaN) use the brute-force loop
     // cold tables
     const RgBodyDev *bodies;
     const RgMatDev *mats;
@@ -92,8 +113,8 @@ struct RgKernelArgs {
     const RgTexDev *texs;
     int32_t n_bodies, n_lights, n_textures;
     // LDS arena (byte offsets; used by the LDS-staged kernel variants)
-    // [sphf | sphf2 | sph | cc | pln | dsk | box | bodies | mats | lights | texs] (byte offsets)
-    uint32_t lds_sph, lds_cc, lds_pln, lds_dsk, lds_box, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
+    // [sphf | sphf2 | sph | cc | nodes | pln | dsk | box | bodies | mats | lights | texs] (byte offsets)
+    uint32_t lds_sph, lds_cc, lds_nodes, lds_pln, lds_dsk, lds_box, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
     int32_t path;            // RG_PATH_* forced by rg_debug_set_path, or RG_PATH_AUTO
     // frame
     uint32_t width, height;

@@ -21,6 +21,7 @@
 #include <type_traits>
 
 #include "../../include/raingun.h"
+#include "rg_bvh_ray.h"
 #include "rg_device.h"
 
 #pragma clang fp contract(off)
@@ -150,6 +151,8 @@ struct SphScalar {
     const RG_CONST RgPln *pl;
     const RG_CONST RgDsk *dk;
     const RG_CONST RgBox *bx;
+    const RG_CONST RgBvhNode *nd;
+    __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
     __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
     __device__ __forceinline__ RgDsk getd(int i) const { return dk[i]; }
     __device__ __forceinline__ RgBox getb(int i) const { return bx[i]; }
@@ -166,6 +169,8 @@ struct SphLds {
     const RgPln *pl;
     const RgDsk *dk;
     const RgBox *bx;
+    const RgBvhNode *nd;
+    __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
     __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
     __device__ __forceinline__ RgDsk getd(int i) const { return dk[i]; }
     __device__ __forceinline__ RgBox getb(int i) const { return bx[i]; }
@@ -390,9 +395,134 @@ __device__ __forceinline__ bool sph_query(const RgKernelArgs &a, const Src &src,
     return __any(need);
 }
 
-template <bool F32F, class Src>
+// ---------------------------------------------------------------- BVH traversal
+// (the tree is built on the host by rg_bvh.cpp.)  The wave
+// walks ONE node at a time: every lane tests the node's child boxes against
+// its own ray (f32 slab test, rg_bvh_ray.h), the wave ballots, a leaf hit by
+// any lane is tested at once by the lanes whose box test passed (f32 sphere
+// pre-filter, then the reference's f64 test), and the internal children hit by
+// any lane are visited depth-first, nearest first by the first active lane's
+// entry distance, through a wave-uniform stack in LDS (one 64-entry stack per
+// wave, written by the first active lane).  Boxes only cull spheres the exact
+// test would reject or whose hit cannot be <= the lane's current best (closest
+// hit) or light distance (shadow), and closest_add is order-independent, so the
+// result and every distance equal the brute-force scan.  Lanes whose ray is
+// outside the boxes' error analysis (rg_bvh_ray_ok) or whose closest-hit query
+// already saw a NaN distance (AABB; nhit must stay exact) use the brute-force
+// loop instead.
+#define RG_BVH_STACK 64
+#define RG_BVH_MAX_WAVES 16   // waves per block on the BVH path (256 * RG_HEAVY_WPS threads)
+__shared__ int rg_bvh_stack[RG_BVH_MAX_WAVES][RG_BVH_STACK];  // allocated only by kernels that traverse
+
+__device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float wave_uniform_f(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+template <class Src>
+__device__ __forceinline__ void leaf_primary(const RgKernelArgs &a, const Src &src, int first, int count, V3 d,
+                                             float dx, float dy, float dz, Closest &c) {
+    for (int j = first; j < first + count; ++j) {
+        if (filter_primary(src.getf(j), src.getf2(j), dx, dy, dz)) {
+            const RgSph s = src.get(j);
+            const double cc = src.getcc(j);
+            const double adj = (s.cx * d.x + s.cy * d.y) + s.cz * d.z;
+            const double opp = cc - adj * adj;
+            double t;
+            if (!(opp > s.r2) && sphere_tail(s.r2, opp, adj, t)) closest_add(c, t, rg_cptr(a.sph_id)[j]);
+        }
+    }
+}
+
+template <class Src>
+__device__ __forceinline__ void leaf_query(const RgKernelArgs &a, const Src &src, int first, int count, V3 o, V3 d,
+                                           const RayF &rf, bool shadow, double ld, Closest &c, bool &occl,
+                                           bool &need) {
+    for (int j = first; j < first + count; ++j) {
+        if (need && filter_general(src.getf(j), src.getf2(j), rf)) {
+            const RgSph s = src.get(j);
+            const double hx = s.cx - o.x, hy = s.cy - o.y, hz = s.cz - o.z;
+            const double adj = (hx * d.x + hy * d.y) + hz * d.z;
+            const double opp = ((hx * hx + hy * hy) + hz * hz) - adj * adj;
+            double t;
+            if (!(opp > s.r2) && sphere_tail(s.r2, opp, adj, t)) {
+                if (shadow) {
+                    if (!(t > ld)) { occl = true; need = false; }
+                } else {
+                    closest_add(c, t, rg_cptr(a.sph_id)[j]);
+                }
+            }
+        }
+    }
+}
+
+// KIND 0: primary ray (o = 0); 1: closest hit; 2: any hit with t <= ld.
+// Called by the lanes that take the BVH (exec mask); `need` drops for a
+// shadow lane at its first occluder.
+template <int KIND, class Src>
+__device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &src, V3 o, V3 d, double ld, Closest &c,
+                                            bool &occl, bool &need) {
+    int *stack = rg_bvh_stack[threadIdx.x >> 6];
+    const RayB rb = rg_make_rayb(o.x, o.y, o.z, d.x, d.y, d.z);
+    RayF rf;
+    const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+    if constexpr (KIND != 0) rf = make_rayf(o, d);
+    const float tld = KIND == 2 ? rg_f32_up(ld) : 0.0f;
+    const int lane = (int)(threadIdx.x & 63u);
+    const bool writer = lane == wave_uniform(lane);
+    int sp = 0;
+    int node = 0;
+    for (;;) {
+        const RgBvhNode N = src.getn(node);
+        const int nch = wave_uniform(N.nchild);
+        const float tb = KIND == 2 ? tld : (c.id >= 0 ? rg_f32_up(c.t) : __builtin_huge_valf());
+        int next = -1;
+        float next_key = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < nch) {
+                float tn = 0.0f;
+                const bool h = need && rg_child_hit(N, k, rb, tb, tn);
+                if (__any(h)) {
+                    const int ch = wave_uniform(N.child[k]);
+                    if (ch < 0) {
+                        const int v = ~ch, first = v >> 3, count = (v & 7) + 1;
+                        if (h) {
+                            if constexpr (KIND == 0) leaf_primary(a, src, first, count, d, dx, dy, dz, c);
+                            else leaf_query(a, src, first, count, o, d, rf, KIND == 2, ld, c, occl, need);
+                        }
+                    } else {
+                        const float key = wave_uniform_f(h ? tn : __builtin_huge_valf());
+                        int push = ch;
+                        if (next < 0 || key < next_key) {
+                            push = next;
+                            next = ch;
+                            next_key = key;
+                        }
+                        if (push >= 0 && sp < RG_BVH_STACK) {
+                            if (writer) stack[sp] = push;
+                            ++sp;
+                        }
+                    }
+                }
+            }
+        }
+        if constexpr (KIND == 2) {
+            if (!__any(need)) return;
+        }
+        if (next >= 0) {
+            node = next;
+        } else {
+            if (sp == 0) return;
+            --sp;
+            node = wave_uniform(stack[sp]);
+        }
+    }
+}
+
+template <bool F32F, bool BVH, class Src>
 __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
-    sph_primary<F32F>(a, src, d, c);
+    if constexpr (!BVH) sph_primary<F32F>(a, src, d, c);
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = src.getp(i);
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137
@@ -416,6 +546,14 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
             if (aabb_hit(b, o, inv, sx, sy, sz, t)) closest_add(c, t, rg_cptr(a.box_id)[i]);
         }
     }
+    if constexpr (BVH) {  // spheres last: the other bodies' hits already bound the search
+        const bool ok = !c.nan && rg_bvh_ray_ok(a.bvh_obound, 0.0, 0.0, 0.0, d.x, d.y, d.z);
+        if (!ok) sph_primary<F32F>(a, src, d, c);
+        if (ok) {
+            bool need = true, unused = false;
+            bvh_spheres<0>(a, src, o, d, 0.0, c, unused, need);
+        }
+    }
 }
 
 // General query: closest-hit for secondary rays, any-hit for shadow rays.
@@ -423,12 +561,14 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
 // !(t > light_distance)  <=>  !(min t > light_distance)  (rendering.rs:152-155),
 // so a lane stops testing at its first such hit and the wave leaves the body
 // loops as soon as every lane that is still testing is a finished shadow ray.
-template <bool F32F, class Src>
+template <bool F32F, bool BVH, class Src>
 __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &src, const Ray &r, bool shadow, double ld,
                                             Closest &c, bool &occl) {
     const V3 o = r.o, d = r.d;
     bool need = true;
-    if (!sph_query<F32F>(a, src, o, d, shadow, ld, c, occl, need)) return;
+    if constexpr (!BVH) {
+        if (!sph_query<F32F>(a, src, o, d, shadow, ld, c, occl, need)) return;
+    }
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = src.getp(i);
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137-148
@@ -469,6 +609,18 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
                     closest_add(c, t, rg_cptr(a.box_id)[i]);
                 }
             }
+        }
+    }
+    if constexpr (BVH) {  // spheres last: plane/disk/box hits already bound the search
+        if (!__any(need)) return;
+        const bool ok = need && !c.nan && rg_bvh_ray_ok(a.bvh_obound, o.x, o.y, o.z, d.x, d.y, d.z);
+        if (need && !ok) {
+            bool nd = true;
+            sph_query<F32F>(a, src, o, d, shadow, ld, c, occl, nd);
+        }
+        if (ok) {
+            if (shadow) bvh_spheres<2>(a, src, o, d, ld, c, occl, need);
+            else bvh_spheres<1>(a, src, o, d, ld, c, occl, need);
         }
     }
 }
@@ -786,8 +938,9 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // repeatedly takes the next 8x8 pixel tile from an atomic queue
 // (counters[16..], sharded) and runs the per-lane state machine until its 64 lanes have
 // written their pixels.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F>
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH>
 __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
+    static_assert(!BVH || 4 * WPS <= RG_BVH_MAX_WAVES, "one BVH stack per wave");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     typename std::conditional<LSPH, SphLds, SphScalar>::type src;
     Cold T;
@@ -795,7 +948,8 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         stage16(smem, a.sphf, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF));
         stage16(smem + (size_t)a.n_sph * sizeof(RgSphF), a.sphf2, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF2));
         stage16(smem + a.lds_sph, a.sph, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSph));
-        stage16(smem + a.lds_cc, a.sph_cc, a.lds_pln - a.lds_cc);
+        stage16(smem + a.lds_cc, a.sph_cc, a.lds_nodes - a.lds_cc);
+        if constexpr (BVH) stage16(smem + a.lds_nodes, a.nodes, (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode));
         stage16(smem + a.lds_pln, a.pln, (uint32_t)a.n_pln * (uint32_t)sizeof(RgPln));
         stage16(smem + a.lds_dsk, a.dsk, (uint32_t)a.n_dsk * (uint32_t)sizeof(RgDsk));
         stage16(smem + a.lds_box, a.box, a.lds_bodies - a.lds_box);
@@ -806,6 +960,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         src.pl = reinterpret_cast<const RgPln *>(smem + a.lds_pln);
         src.dk = reinterpret_cast<const RgDsk *>(smem + a.lds_dsk);
         src.bx = reinterpret_cast<const RgBox *>(smem + a.lds_box);
+        src.nd = reinterpret_cast<const RgBvhNode *>(smem + a.lds_nodes);
     } else {
         src.s = rg_cptr(a.sph);
         src.cc = rg_cptr(a.sph_cc);
@@ -814,6 +969,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         src.pl = rg_cptr(a.pln);
         src.dk = rg_cptr(a.dsk);
         src.bx = rg_cptr(a.box);
+        src.nd = rg_cptr(a.nodes);
     }
     if constexpr (LCOLD) {
         stage16(smem + a.lds_bodies, a.bodies, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgBodyDev));
@@ -906,7 +1062,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             q.o = v3(0.0, 0.0, 0.0);
             q.d = normalize(v3(sx, sy, -1.0));
             n_prim++;
-            trace_primary<F32F>(a, src, q.d, c);
+            trace_primary<F32F, BVH>(a, src, q.d, c);
             mode = MODE_CLOSEST;
             qdepth = 0;
         }
@@ -1150,7 +1306,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                     Ray r1;
                     r1.o = q.o;
                     r1.d = mode == MODE_SHADOW ? sb.d[0] : q.d;
-                    trace_query<F32F>(a, src, r1, mode == MODE_SHADOW, sb.ld[0], c, o1);
+                    trace_query<F32F, BVH>(a, src, r1, mode == MODE_SHADOW, sb.ld[0], c, o1);
                     occl = o1 ? 1u : 0u;
                 }
             } else {
@@ -1159,7 +1315,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                 if (mode == MODE_CLOSEST) {
 #ifndef RG_DBG_NO_SEC_TRACE
                     bool unused = false;
-                    trace_query<F32F>(a, src, q, false, 0.0, c, unused);
+                    trace_query<F32F, BVH>(a, src, q, false, 0.0, c, unused);
 #endif
                 }
                 if (mode == MODE_SHADOW) {
@@ -1199,9 +1355,10 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
     bool occl = false;
     if (alive) {
         SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc), rg_cptr(a.sphf), rg_cptr(a.sphf2),
-                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box)};
-        if (a.path == RG_PATH_HEAVY) trace_query<true>(a, src, r, false, 0.0, c, occl);
-        else trace_query<false>(a, src, r, false, 0.0, c, occl);
+                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes)};
+        if (a.n_nodes > 0) trace_query<true, true>(a, src, r, false, 0.0, c, occl);
+        else if (a.path == RG_PATH_HEAVY) trace_query<true, false>(a, src, r, false, 0.0, c, occl);
+        else trace_query<false, false>(a, src, r, false, 0.0, c, occl);
         if (c.nan && c.nhit >= 2) raise_error(a, i, RG_ERR_NAN_DISTANCE);
         dist[i] = c.id >= 0 ? c.t : 0.0;
         body[i] = c.id;
@@ -1211,11 +1368,11 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
 // ---------------------------------------------------------------- launchers
 // One persistent block per CU slot: grid = CUs x (blocks per CU the register
 // and LDS budgets admit), capped by the tiles the frame has.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F>
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH>
 static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream) {
     static int cus = 0, per_cu = 0;
     static size_t lds_cached = ~(size_t)0;
-    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F>;
+    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH>;
     if (cus == 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
@@ -1253,13 +1410,15 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
 #define RG_HEAVY_SCENE_BODIES 32         // bodies per ray at which the trace loop, not shading, dominates
 #endif
 
-template <int MAXD, int WPS, int LB, bool F32F>
+template <int MAXD, int WPS, int LB, bool F32F, bool BVH>
 static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream) {
-    if (a->lds_total_bytes <= RG_LDS_BUDGET)  // whole scene (empty sphere part if n_sph == 0)
-        return launch_one<MAXD, true, true, WPS, LB, F32F>(a, a->lds_total_bytes, stream);
-    if (a->n_sph > 0 && a->lds_hot_bytes <= RG_LDS_BUDGET)
-        return launch_one<MAXD, true, false, WPS, LB, F32F>(a, a->lds_hot_bytes, stream);
-    return launch_one<MAXD, false, false, WPS, LB, F32F>(a, 0, stream);
+    // the BVH kernels also hold the static per-wave traversal stacks
+    constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u);
+    if (a->lds_total_bytes <= budget)  // whole scene (empty sphere part if n_sph == 0)
+        return launch_one<MAXD, true, true, WPS, LB, F32F, BVH>(a, a->lds_total_bytes, stream);
+    if (a->n_sph > 0 && a->lds_hot_bytes <= budget)
+        return launch_one<MAXD, true, false, WPS, LB, F32F, BVH>(a, a->lds_hot_bytes, stream);
+    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH>(a, 0, stream);
 }
 
 #ifndef RG_LIGHT_WPS
@@ -1278,8 +1437,9 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
 #endif
     if (a->path != RG_PATH_AUTO) heavy = a->path == RG_PATH_HEAVY;
     if (a->n_lights > RG_LB) heavy = true;  // the light path shades all lights in ONE batch
-    return heavy ? launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER>(a, stream)
-                 : launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false>(a, stream);
+    if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false>(a, stream);
+    if (a->n_nodes > 0) return launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true>(a, stream);
+    return launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false>(a, stream);
 }
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {

@@ -239,7 +239,7 @@ class SceneDesc:
 class DeviceScene:
     """An rg_scene handle: the scene uploaded to one GPU."""
 
-    def __init__(self, scene: "Scene", device: int = 0, path: Optional[int] = None):
+    def __init__(self, scene: "Scene", device: int = 0, path: Optional[int] = None, bvh: Optional[bool] = None):
         self._desc = SceneDesc(scene)
         h = C.c_void_p()
         _abi.check(_abi.lib().rg_scene_create(self._desc.ptr(), int(device), C.byref(h)), "rg_scene_create")
@@ -247,6 +247,8 @@ class DeviceScene:
         self.device = device
         if path is not None:
             self.set_path(path)
+        if bvh is not None:
+            self.set_bvh(bvh)
 
     def close(self) -> None:
         if getattr(self, "handle", None):
@@ -262,6 +264,15 @@ class DeviceScene:
     def set_path(self, path: int) -> None:
         """Force a kernel path (_abi.PATH_AUTO / PATH_LIGHT / PATH_HEAVY; include/raingun_debug.h)."""
         _abi.check(_abi.lib().rg_debug_set_path(self.handle, int(path)))
+
+    def set_bvh(self, enable: bool) -> None:
+        """Use (default) or bypass the sphere BVH (include/raingun_debug.h)."""
+        _abi.check(_abi.lib().rg_debug_set_bvh(self.handle, 1 if enable else 0))
+
+    def bvh_info(self) -> _abi.rg_bvh_info:
+        info = _abi.rg_bvh_info()
+        _abi.check(_abi.lib().rg_debug_bvh_info(self.handle, C.byref(info)))
+        return info
 
     def set_max_depth(self, depth: int) -> None:
         _abi.check(_abi.lib().rg_scene_set_max_depth(self.handle, int(depth)))

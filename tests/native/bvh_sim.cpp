@@ -1,0 +1,227 @@
+// bvh_sim.cpp — CPU check that the sphere BVH (raingun_amd/csrc/rg_bvh.cpp)
+// never culls a sphere the exact reference test would accept: every ray's
+// closest hit (t, YAML index) and any-hit shadow answer via BVH traversal must
+// equal the brute-force scan.  The traversal uses the kernel's own slab test
+// (rg_bvh_ray.h).  Built and run by tests/test_bvh_cpu.py.
+//
+// usage: bvh_sim [n_rays_per_kind] < spheres.txt   (n, then n lines "cx cy cz r")
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../raingun_amd/csrc/rg_bvh.h"
+#include "../../raingun_amd/csrc/rg_bvh_ray.h"
+
+struct Hit { double t; int id; };
+
+// bodies.rs:92-119 (f64, unfused; compiled with -ffp-contract=off)
+static bool sphere_exact(const double *s, const double o[3], const double d[3], double &t) {
+    const double hx = s[0] - o[0], hy = s[1] - o[1], hz = s[2] - o[2];
+    const double adj = (hx * d[0] + hy * d[1]) + hz * d[2];
+    const double opp = ((hx * hx + hy * hy) + hz * hz) - adj * adj;
+    const double r2 = s[3] * s[3];
+    if (opp > r2) return false;
+    const double th = std::sqrt(r2 - opp);
+    const double d0 = adj - th, d1 = adj + th;
+    if (d0 < 0.0 && d1 < 0.0) return false;
+    t = d0 < 0.0 ? d1 : (d1 < 0.0 ? d0 : std::fmin(d0, d1));
+    return true;
+}
+static void add(Hit &h, double t, int id) {
+    if (h.id < 0 || t < h.t || (t == h.t && id < h.id)) { h.t = t; h.id = id; }
+}
+
+struct Scene {
+    std::vector<double> sp;      // input order, 4 per sphere
+    RgBvhBuild bvh;
+    std::vector<double> sp_bvh;  // BVH order
+};
+
+static Hit brute(const Scene &S, const double o[3], const double d[3]) {
+    Hit h{0.0, -1};
+    const int n = (int)S.sp.size() / 4;
+    for (int i = 0; i < n; ++i) {
+        double t;
+        if (sphere_exact(&S.sp[4 * i], o, d, t)) add(h, t, i);
+    }
+    return h;
+}
+static bool brute_any(const Scene &S, const double o[3], const double d[3], double ld) {
+    const int n = (int)S.sp.size() / 4;
+    for (int i = 0; i < n; ++i) {
+        double t;
+        if (sphere_exact(&S.sp[4 * i], o, d, t) && !(t > ld)) return true;
+    }
+    return false;
+}
+
+static long g_tests = 0, g_nodes = 0;
+
+// shadow: ld >= 0 -> any-hit within ld; ld < 0 -> closest hit
+static Hit bvh_trace(const Scene &S, const double o[3], const double d[3], double ld, bool &any) {
+    const RayB rb = rg_make_rayb(o[0], o[1], o[2], d[0], d[1], d[2]);
+    Hit h{0.0, -1};
+    any = false;
+    const bool shadow = ld >= 0.0;
+    int stack[64], sp = 0, node = 0;
+    for (;;) {
+        const RgBvhNode &N = S.bvh.nodes[node];
+        ++g_nodes;
+        const float tb = shadow ? rg_f32_up(ld) : (h.id >= 0 ? rg_f32_up(h.t) : HUGE_VALF);
+        int kids[4], nk = 0;
+        float keys[4];
+        for (int k = 0; k < N.nchild; ++k) {
+            float tn;
+            if (!rg_child_hit(N, k, rb, tb, tn)) continue;
+            if (N.child[k] < 0) {
+                const int v = ~N.child[k], first = v >> 3, count = (v & 7) + 1;
+                for (int j = first; j < first + count; ++j) {
+                    double t;
+                    ++g_tests;
+                    if (sphere_exact(&S.sp_bvh[4 * j], o, d, t)) {
+                        if (shadow) { if (!(t > ld)) { any = true; return h; } }
+                        else add(h, t, (int)S.bvh.order[j]);
+                    }
+                }
+            } else {
+                kids[nk] = N.child[k];
+                keys[nk++] = tn;
+            }
+        }
+        if (nk == 0) {
+            if (sp == 0) break;
+            node = stack[--sp];
+            continue;
+        }
+        for (int i = 1; i < nk; ++i)  // ascending entry distance
+            for (int j = i; j > 0 && keys[j] < keys[j - 1]; --j) {
+                std::swap(keys[j], keys[j - 1]);
+                std::swap(kids[j], kids[j - 1]);
+            }
+        for (int i = nk - 1; i >= 1; --i) {
+            if (sp >= 64) { std::fprintf(stderr, "stack overflow\n"); std::exit(3); }
+            stack[sp++] = kids[i];
+        }
+        node = kids[0];
+    }
+    return h;
+}
+
+static uint64_t rng_state = 0x5EEDULL;
+static double urand() {  // SplitMix64 -> [0, 1)
+    uint64_t z = (rng_state += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
+static void unit(double v[3]) {
+    const double inv = 1.0 / std::sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+    v[0] *= inv; v[1] *= inv; v[2] *= inv;
+}
+static void rand_dir(double v[3]) {
+    do { for (int k = 0; k < 3; ++k) v[k] = 2.0 * urand() - 1.0; } while ((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2] < 1e-6);
+    unit(v);
+}
+
+int main(int argc, char **argv) {
+    const long per_kind = argc > 1 ? std::atol(argv[1]) : 20000;
+    int n = 0;
+    if (std::scanf("%d", &n) != 1 || n < 2) { std::fprintf(stderr, "bad input\n"); return 2; }
+    Scene S;
+    S.sp.resize(4 * (size_t)n);
+    for (int i = 0; i < 4 * n; ++i)
+        if (std::scanf("%lf", &S.sp[i]) != 1) { std::fprintf(stderr, "bad sphere\n"); return 2; }
+    if (!rg_build_bvh(S.sp.data(), n, S.bvh)) { std::fprintf(stderr, "build failed\n"); return 2; }
+    S.sp_bvh.resize(S.sp.size());
+    for (int j = 0; j < n; ++j) std::memcpy(&S.sp_bvh[4 * j], &S.sp[4 * S.bvh.order[j]], 32);
+    // structural checks: every sphere in exactly one leaf, leaf boxes contain it
+    if (!std::getenv("BVH_SIM_SKIP_STRUCT")) {
+    std::vector<int> seen(n, 0);
+    for (const RgBvhNode &N : S.bvh.nodes)
+        for (int k = 0; k < N.nchild; ++k)
+            if (N.child[k] < 0) {
+                const int v = ~N.child[k], first = v >> 3, count = (v & 7) + 1;
+                for (int j = first; j < first + count; ++j) {
+                    ++seen[j];
+                    const double *s = &S.sp_bvh[4 * j];
+                    const double r = std::fabs(s[3]);
+                    if (!(N.lox[k] <= s[0] - r && N.hix[k] >= s[0] + r && N.loy[k] <= s[1] - r && N.hiy[k] >= s[1] + r &&
+                          N.loz[k] <= s[2] - r && N.hiz[k] >= s[2] + r)) { std::fprintf(stderr, "leaf box\n"); return 1; }
+                }
+            }
+    for (int j = 0; j < n; ++j) if (seen[j] != 1) { std::fprintf(stderr, "leaf cover\n"); return 1; }
+    }
+
+    long rays = 0, fallback = 0, mism = 0, hits = 0, shadow_rays = 0, occluded = 0;
+    const double O = S.bvh.obound;
+    auto check = [&](const double o[3], const double d[3]) {
+        ++rays;
+        if (!rg_bvh_ray_ok(S.bvh.obound, o[0], o[1], o[2], d[0], d[1], d[2])) { ++fallback; return; }
+        bool any;
+        const Hit b = brute(S, o, d), v = bvh_trace(S, o, d, -1.0, any);
+        if (b.id != v.id || (b.id >= 0 && std::memcmp(&b.t, &v.t, 8) != 0)) {
+            if (++mism <= 5)
+                std::fprintf(stderr, "closest mismatch o=(%.17g %.17g %.17g) d=(%.17g %.17g %.17g) brute %d %.17g bvh %d %.17g\n",
+                             o[0], o[1], o[2], d[0], d[1], d[2], b.id, b.t, v.id, v.t);
+        }
+        hits += b.id >= 0;
+        const double lds[3] = {b.id >= 0 ? b.t : 10.0, urand() * 60.0, HUGE_VAL};
+        for (double ld : lds) {
+            ++shadow_rays;
+            const bool ba = brute_any(S, o, d, ld);
+            bvh_trace(S, o, d, ld, any);
+            occluded += ba;
+            if (ba != any && ++mism <= 5) std::fprintf(stderr, "shadow mismatch ld=%.17g\n", ld);
+        }
+    };
+    double o[3], d[3];
+    // 1. primary rays (ray.rs:37-54 at 3840x2160, fov 90, sampled pixels)
+    for (long i = 0; i < per_kind; ++i) {
+        const double x = std::floor(urand() * 3840), y = std::floor(urand() * 2160);
+        const double sx = (((x + 0.5) / 3840.0) * 2.0 - 1.0) * (3840.0 / 2160.0) * std::tan(90.0 * (M_PI / 180.0) / 2.0);
+        const double sy = (1.0 - ((y + 0.5) / 2160.0) * 2.0) * std::tan(90.0 * (M_PI / 180.0) / 2.0);
+        o[0] = o[1] = o[2] = 0.0;
+        d[0] = sx; d[1] = sy; d[2] = -1.0;
+        unit(d);
+        check(o, d);
+    }
+    // 2. secondary/shadow-like rays from sphere surfaces (hit + n * 1e-13)
+    for (long i = 0; i < per_kind; ++i) {
+        const double *s = &S.sp[4 * (size_t)(urand() * n)];
+        double nrm[3];
+        rand_dir(nrm);
+        for (int k = 0; k < 3; ++k) o[k] = s[k] + nrm[k] * std::fabs(s[3]) + nrm[k] * 1e-13;
+        rand_dir(d);
+        check(o, d);
+    }
+    // 3. grazing rays: offset r(1 +- eps) from a sphere centre, perpendicular to d
+    const double eps[4] = {1e-9, -1e-9, 1e-13, -1e-13};
+    for (long i = 0; i < per_kind; ++i) {
+        const double *s = &S.sp[4 * (size_t)(urand() * n)];
+        rand_dir(d);
+        double p[3];
+        rand_dir(p);
+        const double pd = (p[0] * d[0] + p[1] * d[1]) + p[2] * d[2];
+        for (int k = 0; k < 3; ++k) p[k] -= pd * d[k];
+        unit(p);
+        const double L = 2.0 + urand() * 60.0, off = std::fabs(s[3]) * (1.0 + eps[i & 3]);
+        for (int k = 0; k < 3; ++k) o[k] = s[k] - d[k] * L + p[k] * off;
+        check(o, d);
+    }
+    // 4. arbitrary origins, up to 1.2x the origin bound (some take the fallback)
+    for (long i = 0; i < per_kind; ++i) {
+        for (int k = 0; k < 3; ++k) o[k] = (2.0 * urand() - 1.0) * 1.2 * O * (urand() < 0.7 ? 0.1 : 1.0);
+        rand_dir(d);
+        check(o, d);
+    }
+    std::printf("{\"spheres\": %d, \"nodes\": %zu, \"leaves\": %d, \"depth\": %d, \"margin\": %.6g, \"obound\": %.6g, "
+                "\"rays\": %ld, \"fallback\": %ld, \"hits\": %ld, \"shadow_rays\": %ld, \"occluded\": %ld, "
+                "\"exact_tests_per_ray\": %.3f, \"nodes_per_ray\": %.3f, \"mismatches\": %ld}\n",
+                n, S.bvh.nodes.size(), S.bvh.leaves, S.bvh.depth, S.bvh.margin, (double)S.bvh.obound, rays, fallback,
+                hits, shadow_rays, occluded, (double)g_tests / (double)(4 * (rays - fallback)),
+                (double)g_nodes / (double)(4 * (rays - fallback)), mism);
+    return mism ? 1 : 0;
+}

@@ -26,9 +26,9 @@ def _device():
     assert lib.rg_device_count() > 0, "no HIP device visible"
 
 
-def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0, path=None):
+def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0, path=None, bvh=None):
     desc = SceneDesc(scene)
-    ds = DeviceScene(scene, path=path)
+    ds = DeviceScene(scene, path=path, bvh=bvh)
     st = _abi.rg_stats()
     g_rgba, g_rgb = ds.render_tiles(w, h, tile_rows, stride, offset, want_rgb=True, stats=st)
     o_st, o_rgba, o_rgb, o_counts, o_err = oracle_lib.render(desc, w, h, tile_rows, stride, offset, want_rgb=True)
@@ -43,6 +43,9 @@ def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0, path=None
 
 
 PATHS = [_abi.PATH_LIGHT, _abi.PATH_HEAVY]  # both kernel paths on every scene
+# (kernel path, sphere BVH): the light path never traverses; the heavy path
+# with >= 16 spheres traverses the BVH by default
+PATH_BVH = [(_abi.PATH_LIGHT, False), (_abi.PATH_HEAVY, False), (_abi.PATH_HEAVY, True)]
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -85,9 +88,36 @@ def test_config3_test3_4k(oracle_lib, example_scenes):
     (200, 2, 2, 160, 90),
     (40, 4, 20, 160, 90),
 ])
-@pytest.mark.parametrize("path", PATHS)
-def test_synthetic(oracle_lib, n, planes, depth, w, h, path):
-    _compare(oracle_lib, synthetic_scene(n, planes, depth), w, h, path=path)
+@pytest.mark.parametrize("path,bvh", PATH_BVH)
+def test_synthetic(oracle_lib, n, planes, depth, w, h, path, bvh):
+    _compare(oracle_lib, synthetic_scene(n, planes, depth), w, h, path=path, bvh=bvh)
+
+
+def test_bvh_is_built_for_sphere_scenes():
+    ds = DeviceScene(synthetic_scene(1024, 2, 5))
+    info = ds.bvh_info()
+    assert info.built == 1 and info.enabled == 1 and info.nodes > 64 and info.leaves >= 1024 // 4
+    assert 0 < info.margin < 0.05 and info.origin_bound > 100
+    ds.set_bvh(False)
+    assert ds.bvh_info().enabled == 0
+    ds.close()
+    small = DeviceScene(synthetic_scene(8, 2, 5))
+    assert small.bvh_info().built == 0
+    small.close()
+
+
+@pytest.mark.parametrize("bvh", [True, False])
+def test_config5_shape_4096_spheres_8_planes(oracle_lib, bvh):
+    """BASELINE configs[4]'s scene (4096 spheres + 8 planes, depth 8; the sphere
+    tables exceed LDS, so the BVH kernel reads nodes through the scalar cache)
+    at a reduced resolution the CPU restatement finishes quickly."""
+    _compare(oracle_lib, synthetic_scene(4096, 8, 8), 256, 144, path=_abi.PATH_HEAVY, bvh=bvh)
+
+
+def test_north_star_scene_4k_bvh(oracle_lib):
+    """The north-star scene (1024 spheres) at the full 3840x2160, depth 5,
+    every 9th 16-row tile (the restatement scans all 1026 bodies per ray)."""
+    _compare(oracle_lib, synthetic_scene(1024, 2, 5), 3840, 2160, 16, 9, 4)
 
 
 def test_odd_sizes_and_square(oracle_lib, example_scenes):
@@ -142,7 +172,8 @@ def test_stream_cancel(example_scenes):
     assert calls == [0]
 
 
-def test_trace_matches_oracle(oracle_lib):
+@pytest.mark.parametrize("bvh", [True, False])
+def test_trace_matches_oracle(oracle_lib, bvh):
     s = synthetic_scene(256, 2, 5)
     rng = np.random.default_rng(7)
     n = 4096
@@ -150,7 +181,7 @@ def test_trace_matches_oracle(oracle_lib):
     d = rng.normal(size=(n, 3))
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     rays = np.concatenate([o, d], axis=1)
-    gd, gb = DeviceScene(s).trace(rays)
+    gd, gb = DeviceScene(s, bvh=bvh).trace(rays)
     st, od, ob = oracle_lib.trace(SceneDesc(s), rays)
     assert st == 0
     assert np.array_equal(gb, ob)
@@ -208,13 +239,13 @@ def test_f32_prefilter_tangent_rays(oracle_lib, scale):
         rays.append(np.concatenate([o, d]))
         targets.append(k)
     rays, targets = np.array(rays), np.array(targets)
-    for path in PATHS:
-        ds = DeviceScene(s, path=path)
+    for path, bvh in PATH_BVH:
+        ds = DeviceScene(s, path=path, bvh=bvh)
         gd, gb = ds.trace(rays)
         ds.close()
         st, od, ob = oracle_lib.trace(SceneDesc(s), rays)
         assert st == 0
-        assert np.array_equal(gb, ob), f"path {path}: {np.count_nonzero(gb != ob)} rays differ"
+        assert np.array_equal(gb, ob), f"path {path} bvh {bvh}: {np.count_nonzero(gb != ob)} rays differ"
         hit = ob >= 0
         assert np.array_equal(gd[hit], od[hit])
     # where nothing else is in the way, grazing rays split between hitting and
