@@ -33,6 +33,11 @@ typedef struct rg_bvh_info {
 rg_status rg_debug_set_bvh(rg_scene *scene, int32_t enable);
 rg_status rg_debug_bvh_info(const rg_scene *scene, rg_bvh_info *info);
 
+/* Copy the scene's 16 statistics words after the last render: [0..2] ray
+ * counts, [4..8] BVH traversal statistics when the library was built with
+ * -DRG_BVH_STATS (zero otherwise). */
+rg_status rg_debug_counters(const rg_scene *scene, uint64_t out[16]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,6 +21,16 @@
 // sum with a margin > 2x, so for every sphere the exact test could accept with
 // t <= best, the computed slab interval of every box on its path is non-empty,
 // has tmax >= 0 and tmin <= best.  Boxes are then rounded outward to f32.
+//
+// The exact test's slack, precisely: with H = c - o, eta = |d|^2 - 1 and
+// gamma ~ 9e-16 (relative error of the few f64 ops in opp), the computed opp is
+// >= p^2 - (eta + 2 gamma)|H|^2 (p = true distance of c from the ray line), so
+// an accepted sphere has p <= r + sqrt(eta + 1.8e-15)|H|, and the computed hit
+// point lies within 3 sqrt(eta + 1.8e-15)|H| of the true (slack-inflated)
+// sphere.  Near rays: |H| <= sqrt(3) O + S and eta <= 1e-13 give <= m/5.  Far
+// origins (rg_bvh_classify) are admitted while that term is <= m/4, and their
+// box tests start at the f64 entry point into [-(S + 2m), S + 2m]^3 so the f32
+// slab bound above still applies.
 #if defined(__HIP__)
 #include <hip/hip_runtime.h>  // hipcc builds this file as HIP (host code only)
 #endif
@@ -231,6 +241,8 @@ bool rg_build_bvh(const double *sp, int n, RgBvhBuild &out) {
     out.order = std::move(b.idx);
     out.obound = f32_down(O);
     out.margin = margin;
+    out.extent = S;
+    out.rbound = S + 2.0 * margin;
     out.depth = c.depth;
     out.leaves = c.leaves;
     out.max_stack = 3 * c.depth;

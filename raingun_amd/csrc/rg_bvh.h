@@ -15,6 +15,8 @@ struct RgBvhBuild {
     std::vector<uint32_t> order;    // BVH position -> index in the input sphere list
     float obound = 0.0f;            // origin bound |o_k| <= obound for which the boxes are conservative
     double margin = 0.0;            // box inflation (scene units)
+    double extent = 0.0;            // S: max |coordinate| of any sphere bound
+    double rbound = 0.0;            // S + 2 margin: region holding every inflated box
     int depth = 0;                  // levels of the 4-wide tree
     int leaves = 0;
     int max_stack = 0;              // worst-case traversal stack entries (3 per level)

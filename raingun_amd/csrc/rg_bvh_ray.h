@@ -66,10 +66,44 @@ __device__ __forceinline__ bool rg_child_hit(const RgBvhNode &N, int k, const Ra
     return tmin <= tmax;
 }
 
-// Rays the boxes are conservative for (NaN anywhere -> false).
+// Rays the boxes are conservative for as they are (NaN anywhere -> false).
 __device__ __forceinline__ bool rg_bvh_ray_ok(float obound, double ox, double oy, double oz, double dx, double dy,
                                               double dz) {
     const double dd = (dx * dx + dy * dy) + dz * dz;
     const double ob = (double)obound;
     return fabs(ox) <= ob && fabs(oy) <= ob && fabs(oz) <= ob && fabs(dd - 1.0) <= 1e-13;
+}
+
+enum { RG_BVH_SCAN = 0, RG_BVH_TRAVERSE = 1, RG_BVH_NO_SPHERE = 2 };
+
+// How a ray meets the sphere BVH.  Near rays (rg_bvh_ray_ok) traverse from o.
+// A far origin (|o_k| > obound) is first clipped, in f64, against the region
+// R = [-rbound, rbound]^3 that holds every inflated sphere box: a ray missing R
+// cannot be accepted by any sphere's exact test (NO_SPHERE); otherwise the box
+// tests run from o' = o + t0s d (|o'_k| <= rbound + m: the f32 slab bound holds)
+// with distances shifted by t0s.  Far rays are allowed only while the exact
+// test's rounding slack, 3 sqrt(||d|^2 - 1| + 1.8e-15) |c - o| (derivation:
+// rg_bvh.cpp), stays below a quarter of the box margin; the rest SCAN.
+__device__ __forceinline__ int rg_bvh_classify(float obound, double rbound, double margin, double extent, double ox,
+                                               double oy, double oz, double dx, double dy, double dz, double &t0s) {
+    t0s = 0.0;
+    if (rg_bvh_ray_ok(obound, ox, oy, oz, dx, dy, dz)) return RG_BVH_TRAVERSE;
+    const double dd = (dx * dx + dy * dy) + dz * dz;
+    const double on = sqrt((ox * ox + oy * oy) + oz * oz);
+    if (!(on <= 1e7) || !(3.0 * sqrt(fabs(dd - 1.0) + 1.8e-15) * (on + 1.7321 * extent) <= 0.25 * margin))
+        return RG_BVH_SCAN;  // also NaN / inf
+    double lo = -HUGE_VAL, hi = HUGE_VAL;
+    const double o3[3] = {ox, oy, oz}, d3[3] = {dx, dy, dz};
+    for (int k = 0; k < 3; ++k) {
+        if (d3[k] == 0.0) {
+            if (fabs(o3[k]) > rbound) return RG_BVH_NO_SPHERE;
+            continue;
+        }
+        const double t1 = (-rbound - o3[k]) / d3[k], t2 = (rbound - o3[k]) / d3[k];
+        lo = fmax(lo, fmin(t1, t2));
+        hi = fmin(hi, fmax(t1, t2));
+    }
+    if (!(hi >= lo) || !(hi >= -margin)) return RG_BVH_NO_SPHERE;
+    t0s = fmax(lo - margin, 0.0);
+    return RG_BVH_TRAVERSE;
 }

@@ -50,6 +50,7 @@ struct rg_scene {
     int32_t n_nodes = 0;
     bool bvh_enabled = true;
     float bvh_obound = 0.0f;
+    double bvh_rbound = 0.0, bvh_margin = 0.0, bvh_extent = 0.0;
     rg_bvh_info bvh_info{};
     unsigned long long *counters = nullptr;  // RG_COUNTER_WORDS words (rg_device.h)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -103,11 +104,11 @@ double fov_adjustment(double fov) { return std::tan(fov * (3.1415926535897932384
 
 void release(rg_scene *s) {
     if (!s) return;
-    hipSetDevice(s->device);
-    for (void *p : s->allocations) hipFree(p);
+    (void)hipSetDevice(s->device);
+    for (void *p : s->allocations) (void)hipFree(p);
     s->allocations.clear();
-    if (s->ev0) hipEventDestroy(s->ev0);
-    if (s->ev1) hipEventDestroy(s->ev1);
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
     delete s;
 }
 
@@ -134,6 +135,12 @@ RgKernelArgs make_args(const rg_scene *s) {
     a.nodes = bvh ? s->nodes : nullptr;
     a.n_nodes = bvh ? s->n_nodes : 0;
     a.bvh_obound = s->bvh_obound;
+    a.bvh_rbound = s->bvh_rbound;
+    a.bvh_margin = s->bvh_margin;
+    a.bvh_extent = s->bvh_extent;
+#ifdef RG_BVH_DEBUG_OBOUND  // timing-only ablation builds (unsafe: skips the origin bound)
+    a.bvh_obound = RG_BVH_DEBUG_OBOUND;
+#endif
     a.bodies = s->bodies;
     a.mats = s->mats;
     a.lights = s->lights;
@@ -305,6 +312,9 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         permute(sph_cc);
         permute(sph_id);
         s->bvh_obound = bvh.obound;
+        s->bvh_rbound = bvh.rbound;
+        s->bvh_margin = bvh.margin;
+        s->bvh_extent = bvh.extent;
         s->bvh_info.built = 1;
         s->bvh_info.nodes = (int32_t)bvh.nodes.size();
         s->bvh_info.leaves = bvh.leaves;
@@ -421,7 +431,7 @@ rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t heig
     if (!ok(hipMemcpyAsync(c, s->counters, sizeof c, hipMemcpyDeviceToHost, st))) return RG_ERR_DEVICE;
     if (!ok(hipStreamSynchronize(st))) return RG_ERR_DEVICE;
     float ms = 0.0f;
-    hipEventElapsedTime(&ms, s->ev0, s->ev1);
+    (void)hipEventElapsedTime(&ms, s->ev0, s->ev1);
     stats->rays.primary = c[0];
     stats->rays.shadow = c[1];
     stats->rays.secondary = c[2];
@@ -444,7 +454,7 @@ rg_status rg_render_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     size_t npx = (size_t)rows * width;
     void *d_rgba = nullptr, *d_rgb = nullptr;
     if (!ok(hipMalloc(&d_rgba, npx * 4 + 4))) return RG_ERR_OUT_OF_MEMORY;
-    if (rgb_out && !ok(hipMalloc(&d_rgb, npx * 12 + 4))) { hipFree(d_rgba); return RG_ERR_OUT_OF_MEMORY; }
+    if (rgb_out && !ok(hipMalloc(&d_rgb, npx * 12 + 4))) { (void)hipFree(d_rgba); return RG_ERR_OUT_OF_MEMORY; }
     rg_stats local;
     rg_stats *sp = stats ? stats : &local;
     rg_status st = rg_render_tiles_async(s, width, height, tiling, (uint8_t *)d_rgba, (float *)d_rgb, nullptr, sp);
@@ -452,8 +462,8 @@ rg_status rg_render_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
         if (!ok(hipMemcpy(rgba_out, d_rgba, npx * 4, hipMemcpyDeviceToHost))) st = RG_ERR_DEVICE;
         if (rgb_out && !ok(hipMemcpy(rgb_out, d_rgb, npx * 12, hipMemcpyDeviceToHost))) st = RG_ERR_DEVICE;
     }
-    hipFree(d_rgba);
-    if (d_rgb) hipFree(d_rgb);
+    (void)hipFree(d_rgba);
+    if (d_rgb) (void)hipFree(d_rgb);
     return st;
 }
 
@@ -513,11 +523,11 @@ rg_status rg_render_stream(const rg_scene *s, uint32_t width, uint32_t height, u
             break;
         }
     }
-    if (stream) hipStreamDestroy(stream);
+    if (stream) (void)hipStreamDestroy(stream);
     for (int i = 0; i < 2; ++i) {
-        if (d_buf[i]) hipFree(d_buf[i]);
-        if (h_buf[i]) hipHostFree(h_buf[i]);
-        if (done[i]) hipEventDestroy(done[i]);
+        if (d_buf[i]) (void)hipFree(d_buf[i]);
+        if (h_buf[i]) (void)hipHostFree(h_buf[i]);
+        if (done[i]) (void)hipEventDestroy(done[i]);
     }
     if (stats) {
         stats->rays = total;
@@ -547,6 +557,13 @@ rg_status rg_debug_bvh_info(const rg_scene *s, rg_bvh_info *info) {
     return RG_OK;
 }
 
+rg_status rg_debug_counters(const rg_scene *s, uint64_t out[16]) {
+    if (!s || !out) return RG_ERR_INVALID_ARGUMENT;
+    if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
+    if (!ok(hipMemcpy(out, s->counters, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost))) return RG_ERR_DEVICE;
+    return RG_OK;
+}
+
 rg_status rg_trace(const rg_scene *s, const double *rays, uint32_t n, double *dist, int32_t *body) {
     if (!s || (n && (!rays || !dist || !body))) return RG_ERR_INVALID_ARGUMENT;
     if (n == 0) return RG_OK;
@@ -565,9 +582,9 @@ rg_status rg_trace(const rg_scene *s, const double *rays, uint32_t n, double *di
                         !ok(hipMemcpy(body, d_body, (size_t)n * 4, hipMemcpyDeviceToHost)) ||
                         !ok(hipMemcpy(c, s->counters, sizeof c, hipMemcpyDeviceToHost))))
         st = RG_ERR_DEVICE;
-    if (d_rays) hipFree(d_rays);
-    if (d_dist) hipFree(d_dist);
-    if (d_body) hipFree(d_body);
+    if (d_rays) (void)hipFree(d_rays);
+    if (d_dist) (void)hipFree(d_dist);
+    if (d_body) (void)hipFree(d_body);
     if (st == RG_OK && c[3] != 0) st = (rg_status)(-(int32_t)((~c[3]) & 0xff));
     return st;
 }

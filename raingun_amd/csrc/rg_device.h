@@ -105,7 +105,10 @@ struct RgKernelArgs {
     // BVH over the spheres (n_nodes == 0: none; brute-force sphere loops)
     const RgBvhNode *nodes;
     int32_t n_nodes;
-    float bvh_obound;        // rays with |o_k| > bvh_obound (or NaN) use the brute-force loop
+    float bvh_obound;        // near-ray origin bound |o_k| (rg_bvh_ray.h)
+    double bvh_rbound;       // far rays: half-size of the region holding every inflated sphere box
+    double bvh_margin;       // box inflation m
+    double bvh_extent;       // S: max |coordinate| of any sphere bound
     // cold tables
     const RgBodyDev *bodies;
     const RgMatDev *mats;

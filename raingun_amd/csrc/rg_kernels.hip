@@ -415,6 +415,25 @@ __device__ __forceinline__ bool sph_query(const RgKernelArgs &a, const Src &src,
 __shared__ int rg_bvh_stack[RG_BVH_MAX_WAVES][RG_BVH_STACK];  // allocated only by kernels that traverse
 
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Diagnostic build (-DRG_BVH_STATS): counters[4..15] = traversals, node visits,
+// leaf visits (per wave), lanes traversing, lanes scanning all spheres (any
+// reason), ... by reason (origin out of bound, |d| not unit, NaN), wave clock
+// cycles in traversals, in full scans, in the whole kernel, waves.
+#ifdef RG_BVH_STATS
+#define RG_STAT(word, v)                                                                        \
+    do {                                                                                        \
+        const unsigned long long rg_stat_v = (unsigned long long)(v);                           \
+        if ((threadIdx.x & 63u) == (unsigned)__builtin_amdgcn_readfirstlane(threadIdx.x & 63u)) \
+            atomicAdd(&a.counters[word], rg_stat_v);                                            \
+    } while (0)
+#define RG_LANES(pred) __builtin_popcountll(__ballot(pred))
+#define RG_CLOCK() ((unsigned long long)wall_clock64())
+#else
+#define RG_STAT(word, v) do { } while (0)
+#define RG_LANES(pred) 0
+#define RG_CLOCK() 0ull
+#endif
 __device__ __forceinline__ float wave_uniform_f(float v) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
@@ -458,24 +477,33 @@ __device__ __forceinline__ void leaf_query(const RgKernelArgs &a, const Src &src
 
 // KIND 0: primary ray (o = 0); 1: closest hit; 2: any hit with t <= ld.
 // Called by the lanes that take the BVH (exec mask); `need` drops for a
-// shadow lane at its first occluder.
+// shadow lane at its first occluder.  The box tests start at o + t0s d
+// (t0s > 0 only for far origins, rg_bvh_classify) and prune against
+// distances shifted by t0s; the exact sphere tests use the ray as given.
+__device__ __forceinline__ float bvh_bound(double v) { return v <= 0.0 ? 0.0f : rg_f32_up(v); }
+
 template <int KIND, class Src>
-__device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &src, V3 o, V3 d, double ld, Closest &c,
-                                            bool &occl, bool &need) {
+__device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &src, V3 o, V3 d, double ld, double t0s,
+                                            Closest &c, bool &occl, bool &need) {
     int *stack = rg_bvh_stack[threadIdx.x >> 6];
-    const RayB rb = rg_make_rayb(o.x, o.y, o.z, d.x, d.y, d.z);
+    const V3 ob = t0s > 0.0 ? add(o, scl(d, t0s)) : o;
+    const RayB rb = rg_make_rayb(ob.x, ob.y, ob.z, d.x, d.y, d.z);
     RayF rf;
     const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
     if constexpr (KIND != 0) rf = make_rayf(o, d);
-    const float tld = KIND == 2 ? rg_f32_up(ld) : 0.0f;
+    const float tld = KIND == 2 ? bvh_bound(ld - t0s) : 0.0f;
     const int lane = (int)(threadIdx.x & 63u);
     const bool writer = lane == wave_uniform(lane);
     int sp = 0;
     int node = 0;
+    RG_STAT(4, 1);
+    RG_STAT(7, RG_LANES(1));
+    [[maybe_unused]] const unsigned long long t_in = RG_CLOCK();
     for (;;) {
+        RG_STAT(5, 1);
         const RgBvhNode N = src.getn(node);
         const int nch = wave_uniform(N.nchild);
-        const float tb = KIND == 2 ? tld : (c.id >= 0 ? rg_f32_up(c.t) : __builtin_huge_valf());
+        const float tb = KIND == 2 ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
         int next = -1;
         float next_key = 0.0f;
 #pragma unroll
@@ -487,6 +515,7 @@ __device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &sr
                     const int ch = wave_uniform(N.child[k]);
                     if (ch < 0) {
                         const int v = ~ch, first = v >> 3, count = (v & 7) + 1;
+                        RG_STAT(6, 1);
                         if (h) {
                             if constexpr (KIND == 0) leaf_primary(a, src, first, count, d, dx, dy, dz, c);
                             else leaf_query(a, src, first, count, o, d, rf, KIND == 2, ld, c, occl, need);
@@ -508,16 +537,17 @@ __device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &sr
             }
         }
         if constexpr (KIND == 2) {
-            if (!__any(need)) return;
+            if (!__any(need)) break;
         }
         if (next >= 0) {
             node = next;
         } else {
-            if (sp == 0) return;
+            if (sp == 0) break;
             --sp;
             node = wave_uniform(stack[sp]);
         }
     }
+    RG_STAT(12, RG_CLOCK() - t_in);
 }
 
 template <bool F32F, bool BVH, class Src>
@@ -548,10 +578,15 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
     }
     if constexpr (BVH) {  // spheres last: the other bodies' hits already bound the search
         const bool ok = !c.nan && rg_bvh_ray_ok(a.bvh_obound, 0.0, 0.0, 0.0, d.x, d.y, d.z);
-        if (!ok) sph_primary<F32F>(a, src, d, c);
+        RG_STAT(8, RG_LANES(!ok));
+        if (!ok) {
+            [[maybe_unused]] const unsigned long long t0 = RG_CLOCK();
+            sph_primary<F32F>(a, src, d, c);
+            RG_STAT(13, RG_CLOCK() - t0);
+        }
         if (ok) {
             bool need = true, unused = false;
-            bvh_spheres<0>(a, src, o, d, 0.0, c, unused, need);
+            bvh_spheres<0>(a, src, o, d, 0.0, 0.0, c, unused, need);
         }
     }
 }
@@ -613,14 +648,28 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
     }
     if constexpr (BVH) {  // spheres last: plane/disk/box hits already bound the search
         if (!__any(need)) return;
-        const bool ok = need && !c.nan && rg_bvh_ray_ok(a.bvh_obound, o.x, o.y, o.z, d.x, d.y, d.z);
-        if (need && !ok) {
+        double t0s = 0.0;
+        const int cls = (need && !c.nan) ? rg_bvh_classify(a.bvh_obound, a.bvh_rbound, a.bvh_margin, a.bvh_extent,
+                                                           o.x, o.y, o.z, d.x, d.y, d.z, t0s)
+                                         : RG_BVH_SCAN;
+        const bool ok = need && cls == RG_BVH_TRAVERSE;
+#ifdef RG_BVH_STATS
+        {
+            RG_STAT(8, RG_LANES(need && cls == RG_BVH_SCAN));
+            RG_STAT(9, RG_LANES(need && cls == RG_BVH_TRAVERSE && t0s > 0.0));
+            RG_STAT(10, RG_LANES(need && cls == RG_BVH_NO_SPHERE));
+            RG_STAT(11, RG_LANES(need && c.nan));
+        }
+#endif
+        if (need && cls == RG_BVH_SCAN) {
+            [[maybe_unused]] const unsigned long long t0 = RG_CLOCK();
             bool nd = true;
             sph_query<F32F>(a, src, o, d, shadow, ld, c, occl, nd);
+            RG_STAT(13, RG_CLOCK() - t0);
         }
         if (ok) {
-            if (shadow) bvh_spheres<2>(a, src, o, d, ld, c, occl, need);
-            else bvh_spheres<1>(a, src, o, d, ld, c, occl, need);
+            if (shadow) bvh_spheres<2>(a, src, o, d, ld, t0s, c, occl, need);
+            else bvh_spheres<1>(a, src, o, d, ld, t0s, c, occl, need);
         }
     }
 }
@@ -989,6 +1038,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     if constexpr (LSPH || LCOLD) __syncthreads();
 
     const int lane = threadIdx.x & 63;
+    [[maybe_unused]] const unsigned long long t_kernel = RG_CLOCK();
     const uint32_t tiles_x = (a.width + 7u) / 8u;
     const uint32_t ntiles = tiles_x * ((a.out_rows + 7u) / 8u);
     const C3 def = c3(a.def[0], a.def[1], a.def[2]);
@@ -1329,6 +1379,8 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         }
     }
 
+    RG_STAT(14, RG_CLOCK() - t_kernel);
+    RG_STAT(15, 1);
     // ray counters: wave reduction, one atomic per wave per class
     unsigned long long p64 = wave_sum(n_prim), s64 = wave_sum(n_shadow), q64 = wave_sum(n_sec);
     if (lane == 0) {

@@ -60,8 +60,12 @@ static bool brute_any(const Scene &S, const double o[3], const double d[3], doub
 static long g_tests = 0, g_nodes = 0;
 
 // shadow: ld >= 0 -> any-hit within ld; ld < 0 -> closest hit
-static Hit bvh_trace(const Scene &S, const double o[3], const double d[3], double ld, bool &any) {
-    const RayB rb = rg_make_rayb(o[0], o[1], o[2], d[0], d[1], d[2]);
+static float bound(double v) { return v <= 0.0 ? 0.0f : rg_f32_up(v); }
+
+static Hit bvh_trace(const Scene &S, const double o[3], const double d[3], double ld, double t0s, bool &any) {
+    const double ob[3] = {o[0] + d[0] * t0s, o[1] + d[1] * t0s, o[2] + d[2] * t0s};
+    const RayB rb = t0s > 0.0 ? rg_make_rayb(ob[0], ob[1], ob[2], d[0], d[1], d[2])
+                              : rg_make_rayb(o[0], o[1], o[2], d[0], d[1], d[2]);
     Hit h{0.0, -1};
     any = false;
     const bool shadow = ld >= 0.0;
@@ -69,7 +73,7 @@ static Hit bvh_trace(const Scene &S, const double o[3], const double d[3], doubl
     for (;;) {
         const RgBvhNode &N = S.bvh.nodes[node];
         ++g_nodes;
-        const float tb = shadow ? rg_f32_up(ld) : (h.id >= 0 ? rg_f32_up(h.t) : HUGE_VALF);
+        const float tb = shadow ? bound(ld - t0s) : (h.id >= 0 ? bound(h.t - t0s) : HUGE_VALF);
         int kids[4], nk = 0;
         float keys[4];
         for (int k = 0; k < N.nchild; ++k) {
@@ -155,13 +159,19 @@ int main(int argc, char **argv) {
     for (int j = 0; j < n; ++j) if (seen[j] != 1) { std::fprintf(stderr, "leaf cover\n"); return 1; }
     }
 
-    long rays = 0, fallback = 0, mism = 0, hits = 0, shadow_rays = 0, occluded = 0;
+    long rays = 0, fallback = 0, mism = 0, hits = 0, shadow_rays = 0, occluded = 0, shifted = 0, nosphere = 0;
     const double O = S.bvh.obound;
     auto check = [&](const double o[3], const double d[3]) {
         ++rays;
-        if (!rg_bvh_ray_ok(S.bvh.obound, o[0], o[1], o[2], d[0], d[1], d[2])) { ++fallback; return; }
-        bool any;
-        const Hit b = brute(S, o, d), v = bvh_trace(S, o, d, -1.0, any);
+        double t0s = 0.0;
+        const int cls = rg_bvh_classify(S.bvh.obound, S.bvh.rbound, S.bvh.margin, S.bvh.extent, o[0], o[1], o[2], d[0],
+                                        d[1], d[2], t0s);
+        if (cls == RG_BVH_SCAN) { ++fallback; return; }
+        shifted += t0s > 0.0;
+        nosphere += cls == RG_BVH_NO_SPHERE;
+        bool any = false;
+        const Hit b = brute(S, o, d);
+        const Hit v = cls == RG_BVH_NO_SPHERE ? Hit{0.0, -1} : bvh_trace(S, o, d, -1.0, t0s, any);
         if (b.id != v.id || (b.id >= 0 && std::memcmp(&b.t, &v.t, 8) != 0)) {
             if (++mism <= 5)
                 std::fprintf(stderr, "closest mismatch o=(%.17g %.17g %.17g) d=(%.17g %.17g %.17g) brute %d %.17g bvh %d %.17g\n",
@@ -172,7 +182,8 @@ int main(int argc, char **argv) {
         for (double ld : lds) {
             ++shadow_rays;
             const bool ba = brute_any(S, o, d, ld);
-            bvh_trace(S, o, d, ld, any);
+            any = false;
+            if (cls != RG_BVH_NO_SPHERE) bvh_trace(S, o, d, ld, t0s, any);
             occluded += ba;
             if (ba != any && ++mism <= 5) std::fprintf(stderr, "shadow mismatch ld=%.17g\n", ld);
         }
@@ -217,11 +228,27 @@ int main(int argc, char **argv) {
         rand_dir(d);
         check(o, d);
     }
+    // 5. far origins (floor points seen at grazing angles): |o| from 1.5 O to 3e4 and beyond 1e7,
+    //    directions towards a random sphere or random
+    for (long i = 0; i < per_kind; ++i) {
+        const double R = O * (1.5 + urand() * (i % 3 == 0 ? 80.0 : 10.0)) * (i % 97 == 0 ? 1e5 : 1.0);
+        rand_dir(o);
+        for (int k = 0; k < 3; ++k) o[k] *= R;
+        if (i & 1) {
+            const double *s = &S.sp[4 * (size_t)(urand() * n)];
+            for (int k = 0; k < 3; ++k) d[k] = s[k] + (urand() - 0.5) * 2.5 * std::fabs(s[3]) - o[k];
+            unit(d);
+        } else {
+            rand_dir(d);
+        }
+        check(o, d);
+    }
     std::printf("{\"spheres\": %d, \"nodes\": %zu, \"leaves\": %d, \"depth\": %d, \"margin\": %.6g, \"obound\": %.6g, "
                 "\"rays\": %ld, \"fallback\": %ld, \"hits\": %ld, \"shadow_rays\": %ld, \"occluded\": %ld, "
+                "\"shifted\": %ld, \"no_sphere\": %ld, "
                 "\"exact_tests_per_ray\": %.3f, \"nodes_per_ray\": %.3f, \"mismatches\": %ld}\n",
                 n, S.bvh.nodes.size(), S.bvh.leaves, S.bvh.depth, S.bvh.margin, (double)S.bvh.obound, rays, fallback,
-                hits, shadow_rays, occluded, (double)g_tests / (double)(4 * (rays - fallback)),
+                hits, shadow_rays, occluded, shifted, nosphere, (double)g_tests / (double)(4 * (rays - fallback)),
                 (double)g_nodes / (double)(4 * (rays - fallback)), mism);
     return mism ? 1 : 0;
 }

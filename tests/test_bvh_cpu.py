@@ -1,6 +1,7 @@
 """CPU check of the sphere BVH (raingun_amd/csrc/rg_bvh.cpp + the kernel's slab
 test rg_bvh_ray.h): tests/native/bvh_sim.cpp traces primary, surface-origin,
-grazing (r(1 +- 1e-9), r(1 +- 1e-13)) and far-origin rays through the BVH and
+grazing (r(1 +- 1e-9), r(1 +- 1e-13)) and far-origin rays (up to 1e5 x the
+scene, through the clipped-start path of rg_bvh_classify) through the BVH and
 through the brute-force reference scan; closest hits (t bits, YAML index) and
 shadow any-hit answers must agree on every ray.  A negative control shrinks the
 boxes and must be caught."""
@@ -50,6 +51,7 @@ def test_bvh_matches_brute_force(sim, args):
     assert rc == 0, err
     assert res["mismatches"] == 0
     assert res["hits"] > 0 and res["occluded"] > 0 and res["fallback"] > 0
+    assert res["shifted"] > 1000 and res["no_sphere"] > 1000  # far origins: clipped start / skipped
     if args[0] >= 1024:  # the point of the structure: a handful of exact tests per ray
         assert res["exact_tests_per_ray"] < 16 and res["nodes_per_ray"] < 16
 
