@@ -47,11 +47,13 @@ def load_workload(name: str):
         scene = load_scene(golden / "examples" / "test1.yml", texture_root=golden)
         scene.max_recursion_depth = 5
         label = "examples/test1.yml 3840x2160 depth 5 (BASELINE configs[1])"
-        src = "reference example scene examples/test1.yml; textures decoded on the host (PIL)"
+        src = ("reference example scene examples/test1.yml; textures decoded by the native host layer "
+               "(libraingun_host.so, jpeg-decoder 0.1.11 rounding)")
     elif name == "test3":
         scene = load_scene(golden / "examples" / "test3.yml", texture_root=golden)
         label = "examples/test3.yml 3840x2160 depth 10 (BASELINE configs[2])"
-        src = "reference example scene examples/test3.yml; textures decoded on the host (PIL)"
+        src = ("reference example scene examples/test3.yml; textures decoded by the native host layer "
+               "(libraingun_host.so, jpeg-decoder 0.1.11 rounding)")
     elif name.startswith("synth"):
         n = int(name[5:] or 1024)
         text = synthetic_yaml(n, 2, 5)
@@ -142,6 +144,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     W, H = args.width, args.height
     ds = DeviceScene(scene, device=local_rank)  # scene + textures uploaded once, resident in HBM
     lib = _abi.lib()
+    bvh = ds.bvh_info()
 
     tiling = rd.tiling(rank, world, TILE_ROWS)
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
@@ -245,8 +248,10 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
             "traffic": traffic,
             "basis": f"reference-equivalent work: {ops_per_ray} FP64 ops per ray (16/sphere, 14/plane, 20/disk, "
                      f"18/aabb; SURVEY.md 8d) x {my_rays} rays per launch / mean rg_render_kernel time (HIP events "
-                     f"on the render stream). On >=32-body scenes the kernel's f32 pre-filter skips most of that "
-                     f"FP64 work exactly, so frac can exceed 1 there",
+                     f"on the render stream)" + (
+                         ". The sphere BVH and f32 pre-filter skip most of that work without changing any result, "
+                         "so frac > 1 measures the algorithmic saving over the brute-force scan, not hardware "
+                         "utilisation (DESIGN.md 4b)" if bvh.enabled else ""),
         },
         "roofline_hbm": {
             "bound": "hbm",
@@ -258,6 +263,9 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
             "basis": f"{alg_bytes} B framebuffer written per launch (+{tex} B of textures, L2/MALL resident)",
         },
     }
+    if bvh.enabled:
+        res["bvh"] = {"nodes": bvh.nodes, "leaves": bvh.leaves, "depth": bvh.depth,
+                      "box_margin": round(bvh.margin, 6), "near_origin_bound": round(bvh.origin_bound, 3)}
     if verified is not None:
         res["verified_against_1_rank_frame"] = verified
     if cpu:

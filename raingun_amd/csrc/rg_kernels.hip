@@ -421,11 +421,13 @@ __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_rea
 // reason), ... by reason (origin out of bound, |d| not unit, NaN), wave clock
 // cycles in traversals, in full scans, in the whole kernel, waves.
 #ifdef RG_BVH_STATS
+// accumulated per wave in LDS (cheap), flushed to counters[] once per wave
+__shared__ unsigned long long rg_stat_lds[RG_BVH_MAX_WAVES][16];
 #define RG_STAT(word, v)                                                                        \
     do {                                                                                        \
         const unsigned long long rg_stat_v = (unsigned long long)(v);                           \
         if ((threadIdx.x & 63u) == (unsigned)__builtin_amdgcn_readfirstlane(threadIdx.x & 63u)) \
-            atomicAdd(&a.counters[word], rg_stat_v);                                            \
+            rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][word] += rg_stat_v;              \
     } while (0)
 #define RG_LANES(pred) __builtin_popcountll(__ballot(pred))
 #define RG_CLOCK() ((unsigned long long)wall_clock64())
@@ -1038,6 +1040,9 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     if constexpr (LSPH || LCOLD) __syncthreads();
 
     const int lane = threadIdx.x & 63;
+#ifdef RG_BVH_STATS
+    if (lane < 16) rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][lane] = 0ull;
+#endif
     [[maybe_unused]] const unsigned long long t_kernel = RG_CLOCK();
     const uint32_t tiles_x = (a.width + 7u) / 8u;
     const uint32_t ntiles = tiles_x * ((a.out_rows + 7u) / 8u);
@@ -1381,6 +1386,9 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
 
     RG_STAT(14, RG_CLOCK() - t_kernel);
     RG_STAT(15, 1);
+#ifdef RG_BVH_STATS
+    if (lane >= 4 && lane < 16) atomicAdd(&a.counters[lane], rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][lane]);
+#endif
     // ray counters: wave reduction, one atomic per wave per class
     unsigned long long p64 = wave_sum(n_prim), s64 = wave_sum(n_shadow), q64 = wave_sum(n_sec);
     if (lane == 0) {

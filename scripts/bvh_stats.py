@@ -26,8 +26,8 @@ for name, (n, planes, depth, w, h) in {"synth1024_4k_d5": (1024, 2, 5, 3840, 216
     rays = st.rays.total()
     out[name] = dict(rays=rays, kernel_ms=round(st.kernel_ms, 3), traversals=trav, lanes_per_traversal=lanes / max(trav, 1),
                      nodes_per_traversal=nodes / max(trav, 1), leaves_per_traversal=leaves / max(trav, 1),
-                     fallback_lanes=fallback, fallback_frac=fallback / max(rays, 1),
-                     fallback_origin=c[9], fallback_dir=c[10], fallback_nan=c[11],
+                     scan_lanes=fallback, scan_frac=fallback / max(rays, 1),
+                     clipped_start_lanes=c[9], no_sphere_lanes=c[10], nan_lanes=c[11],
                      clock_traversal_frac=c[12] / max(c[14], 1), clock_fullscan_frac=c[13] / max(c[14], 1),
                      waves=c[15])
     ds.close()
