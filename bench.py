@@ -150,7 +150,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
     slot = rd.slot_rows(H, world, TILE_ROWS)  # equal-size gather slots (last ranks zero-padded)
     out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
-    gathered = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    gathered = rd.gather_buffers(out, world) if (world > 1 and rank == 0) else None
     frame = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
 
     stream = torch.cuda.current_stream(dev)

@@ -33,6 +33,12 @@ typedef struct rg_bvh_info {
 rg_status rg_debug_set_bvh(rg_scene *scene, int32_t enable);
 rg_status rg_debug_bvh_info(const rg_scene *scene, rg_bvh_info *info);
 
+/* Tile scheduling: 1 = a primary-ray probe orders each frame's 8x8 tiles by
+ * estimated cost, most expensive first (stable within a cost class);
+ * 0 = raster order; -1 (default) = ordered on the heavy (trace-dominated)
+ * path only.  Results are identical either way. */
+rg_status rg_debug_set_tile_order(rg_scene *scene, int32_t mode);
+
 /* Copy the scene's 16 statistics words after the last render: [0..2] ray
  * counts, [4..8] BVH traversal statistics when the library was built with
  * -DRG_BVH_STATS (zero otherwise). */

@@ -130,7 +130,8 @@ EXPORTED_SYMBOLS = (
     "rg_trace",
 )
 # include/raingun_debug.h
-DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters")
+DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
+                 "rg_debug_set_tile_order")
 PATH_AUTO, PATH_LIGHT, PATH_HEAVY = -1, 0, 1
 
 
@@ -177,6 +178,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_set_bvh.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_bvh_info.restype = C.c_int32
     lib.rg_debug_bvh_info.argtypes = [C.c_void_p, P(rg_bvh_info)]
+    lib.rg_debug_set_tile_order.restype = C.c_int32
+    lib.rg_debug_set_tile_order.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_counters.restype = C.c_int32
     lib.rg_debug_counters.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.rg_trace.restype = C.c_int32

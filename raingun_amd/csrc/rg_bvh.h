@@ -12,6 +12,8 @@
 
 struct RgBvhBuild {
     std::vector<RgBvhNode> nodes;   // nodes[0] is the root
+    std::vector<RgBvhLane> lane;    // threaded binary layout of the same tree (sphere leaves: filter
+                                    // fields left for the caller, which owns the f32 records)
     std::vector<uint32_t> order;    // BVH position -> index in the input sphere list
     float obound = 0.0f;            // origin bound |o_k| <= obound for which the boxes are conservative
     double margin = 0.0;            // box inflation (scene units)

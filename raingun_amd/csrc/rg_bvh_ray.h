@@ -66,6 +66,16 @@ __device__ __forceinline__ bool rg_child_hit(const RgBvhNode &N, int k, const Ra
     return tmin <= tmax;
 }
 
+// Slab test of one box (threaded layout), same expressions as rg_child_hit.
+__device__ __forceinline__ bool rg_box_hit(const float lo[3], const float hi[3], const RayB &r, float tb) {
+    const float tx1 = RG_FMAF(lo[0], r.ix, -r.oix), tx2 = RG_FMAF(hi[0], r.ix, -r.oix);
+    const float ty1 = RG_FMAF(lo[1], r.iy, -r.oiy), ty2 = RG_FMAF(hi[1], r.iy, -r.oiy);
+    const float tz1 = RG_FMAF(lo[2], r.iz, -r.oiz), tz2 = RG_FMAF(hi[2], r.iz, -r.oiz);
+    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fmaxf(fminf(tz1, tz2), 0.0f));
+    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fminf(fmaxf(tz1, tz2), tb));
+    return tmin <= tmax;
+}
+
 // Rays the boxes are conservative for as they are (NaN anywhere -> false).
 __device__ __forceinline__ bool rg_bvh_ray_ok(float obound, double ox, double oy, double oz, double dx, double dy,
                                               double dz) {

@@ -23,6 +23,8 @@
 #endif
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream);
+extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scratch, uint32_t *perm, hipStream_t stream);
+extern "C" size_t rg_tile_order_scratch_words(uint32_t ntiles);
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,
                                       int32_t *body, hipStream_t stream);
 
@@ -48,11 +50,19 @@ struct rg_scene {
     RgTexDev *texs = nullptr;
     RgBvhNode *nodes = nullptr;  // sphere BVH (sphere tables are in its leaf order)
     int32_t n_nodes = 0;
+    RgBvhLane *lane_nodes = nullptr;  // the same tree, threaded for per-lane traversal
+    int32_t n_lane_nodes = 0;
     bool bvh_enabled = true;
     float bvh_obound = 0.0f;
     double bvh_rbound = 0.0, bvh_margin = 0.0, bvh_extent = 0.0;
     rg_bvh_info bvh_info{};
     unsigned long long *counters = nullptr;  // RG_COUNTER_WORDS words (rg_device.h)
+#ifndef RG_TILE_ORDER
+#define RG_TILE_ORDER -1
+#endif
+    int tile_order = RG_TILE_ORDER;  // expensive tiles first (rg_kernels.hip "tile ordering"): -1 auto (heavy path), 0, 1
+    mutable uint32_t *tile_cost = nullptr, *tile_perm = nullptr;  // probe/sort scratch (rg_launch_tile_order), order
+    mutable size_t tile_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -107,6 +117,8 @@ void release(rg_scene *s) {
     (void)hipSetDevice(s->device);
     for (void *p : s->allocations) (void)hipFree(p);
     s->allocations.clear();
+    if (s->tile_cost) (void)hipFree(s->tile_cost);
+    if (s->tile_perm) (void)hipFree(s->tile_perm);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     delete s;
@@ -134,6 +146,8 @@ RgKernelArgs make_args(const rg_scene *s) {
     const bool bvh = s->bvh_enabled && s->n_nodes > 0;
     a.nodes = bvh ? s->nodes : nullptr;
     a.n_nodes = bvh ? s->n_nodes : 0;
+    a.lane_nodes = bvh ? s->lane_nodes : nullptr;
+    a.n_lane_nodes = bvh ? s->n_lane_nodes : 0;
     a.bvh_obound = s->bvh_obound;
     a.bvh_rbound = s->bvh_rbound;
     a.bvh_margin = s->bvh_margin;
@@ -153,7 +167,8 @@ RgKernelArgs make_args(const rg_scene *s) {
     a.lds_sph = (uint32_t)s->n_sph * (uint32_t)(sizeof(RgSphF) + sizeof(RgSphF2));
     a.lds_cc = a.lds_sph + (uint32_t)s->n_sph * (uint32_t)sizeof(RgSph);
     a.lds_nodes = al16(a.lds_cc + (uint32_t)s->n_sph * 8u);
-    a.lds_pln = a.lds_nodes + (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode);
+    a.lds_lane = a.lds_nodes + (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode);
+    a.lds_pln = a.lds_lane + (uint32_t)a.n_lane_nodes * (uint32_t)sizeof(RgBvhLane);
     a.lds_dsk = a.lds_pln + (uint32_t)s->n_pln * (uint32_t)sizeof(RgPln);
     a.lds_box = a.lds_dsk + (uint32_t)s->n_dsk * (uint32_t)sizeof(RgDsk);
     a.lds_bodies = al16(a.lds_box + (uint32_t)s->n_box * (uint32_t)sizeof(RgBox));
@@ -311,6 +326,15 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         permute(sphf2);
         permute(sph_cc);
         permute(sph_id);
+        for (RgBvhLane &l : bvh.lane) {  // sphere leaves carry their f32 pre-filter record
+            if (l.sph < 0) continue;
+            l.a[0] = sphf[l.sph].cx;
+            l.a[1] = sphf[l.sph].cy;
+            l.a[2] = sphf[l.sph].cz;
+            l.b[0] = sphf[l.sph].r2hi;
+            l.b[1] = sphf2[l.sph].cchi;
+            l.b[2] = 0.0f;
+        }
         s->bvh_obound = bvh.obound;
         s->bvh_rbound = bvh.rbound;
         s->bvh_margin = bvh.margin;
@@ -366,8 +390,10 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
     RG_UP(mats, mats);
     RG_UP(lights, lights);
     RG_UP(nodes, bvh.nodes);
+    RG_UP(lane_nodes, bvh.lane);
 #undef RG_UP
     s->n_nodes = (int32_t)bvh.nodes.size();
+    s->n_lane_nodes = (int32_t)bvh.lane.size();
     // textures: RGBA8 -> one u32 per texel (one 4-byte gather per lookup)
     std::vector<RgTexDev> texs(d->n_textures);
     for (uint32_t i = 0; st == RG_OK && i < d->n_textures; ++i) {
@@ -422,8 +448,23 @@ rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t heig
     a.rgba = reinterpret_cast<uint32_t *>(rgba_dev);
     a.rgb = rgb_dev;
     if (!ok(hipMemsetAsync(s->counters, 0, RG_COUNTER_WORDS * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
+    if (stats && !ok(hipEventRecord(s->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
+    if (s->tile_order == 1 || (s->tile_order < 0 && rg_heavy_path(a))) {
+        const size_t ntiles = (size_t)((width + 7u) / 8u) * ((out_rows + 7u) / 8u);
+        if (ntiles > s->tile_cap) {
+            if (s->tile_cost) (void)hipFree(s->tile_cost);
+            if (s->tile_perm) (void)hipFree(s->tile_perm);
+            s->tile_cost = s->tile_perm = nullptr;
+            s->tile_cap = 0;
+            if (!ok(hipMalloc(&s->tile_cost, rg_tile_order_scratch_words((uint32_t)ntiles) * 4)) ||
+                !ok(hipMalloc(&s->tile_perm, ntiles * 4)))
+                return RG_ERR_OUT_OF_MEMORY;
+            s->tile_cap = ntiles;
+        }
+        if (!ok(rg_launch_tile_order(&a, s->tile_cost, s->tile_perm, st))) return RG_ERR_DEVICE;
+        a.tile_perm = s->tile_perm;
+    }
     if (out_rows == 0) return RG_OK;
-    if (stats && !ok(hipEventRecord(s->ev0, st))) return RG_ERR_DEVICE;
     if (!ok(rg_launch_render(&a, frames_needed(s->max_depth), st))) return RG_ERR_DEVICE;
     if (!stats) return RG_OK;
     if (!ok(hipEventRecord(s->ev1, st))) return RG_ERR_DEVICE;
@@ -554,6 +595,12 @@ rg_status rg_debug_bvh_info(const rg_scene *s, rg_bvh_info *info) {
     if (!s || !info) return RG_ERR_INVALID_ARGUMENT;
     *info = s->bvh_info;
     info->enabled = s->bvh_enabled && s->n_nodes > 0;
+    return RG_OK;
+}
+
+rg_status rg_debug_set_tile_order(rg_scene *s, int32_t mode) {
+    if (!s || mode < -1 || mode > 1) return RG_ERR_INVALID_ARGUMENT;
+    s->tile_order = mode;
     return RG_OK;
 }
 

@@ -19,6 +19,7 @@
 
 #if !defined(__HIP__) && !defined(__HIPCC__)  // plain C++ (host-only builds and tests of rg_bvh.cpp)
 #define __device__
+#define __host__
 #define __forceinline__ inline
 #endif
 
@@ -52,6 +53,18 @@ struct alignas(16) RgBvhNode {
     int32_t child[4];
     int32_t nchild;        // valid children (2..4)
     int32_t pad[3];
+};
+
+// Threaded (stackless) binary BVH for per-lane traversal of incoherent rays:
+// nodes in DFS preorder, the first child of an internal node is the next
+// node, `miss` is where to go when a subtree is skipped (-1: done).  Internal
+// nodes hold the same conservative f32 box as the 4-wide tree (sph = -1);
+// leaf nodes are single spheres carrying their f32 pre-filter record.
+struct alignas(16) RgBvhLane {
+    float a[3];       // internal: box lo     | sphere: f32 centre (RgSphF cx, cy, cz)
+    float b[3];       // internal: box hi     | sphere: {r2hi, cchi, 0}
+    int32_t miss;     // next node when this one is missed / finished
+    int32_t sph;      // -1 internal; else the sphere's row in the (BVH-ordered) sphere tables
 };
 
 struct RgBodyDev {         // per body, YAML order
@@ -105,6 +118,8 @@ struct RgKernelArgs {
     // BVH over the spheres (n_nodes == 0: none; brute-force sphere loops)
     const RgBvhNode *nodes;
     int32_t n_nodes;
+    const RgBvhLane *lane_nodes;   // same spheres, threaded binary layout (per-lane traversal)
+    int32_t n_lane_nodes;
     float bvh_obound;        // near-ray origin bound |o_k| (rg_bvh_ray.h)
     double bvh_rbound;       // far rays: half-size of the region holding every inflated sphere box
     double bvh_margin;       // box inflation m
@@ -116,8 +131,8 @@ struct RgKernelArgs {
     const RgTexDev *texs;
     int32_t n_bodies, n_lights, n_textures;
     // LDS arena (byte offsets; used by the LDS-staged kernel variants)
-    // [sphf | sphf2 | sph | cc | nodes | pln | dsk | box | bodies | mats | lights | texs] (byte offsets)
-    uint32_t lds_sph, lds_cc, lds_nodes, lds_pln, lds_dsk, lds_box, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
+    // [sphf | sphf2 | sph | cc | nodes | lane nodes | pln | dsk | box | bodies | mats | lights | texs] (byte offsets)
+    uint32_t lds_sph, lds_cc, lds_nodes, lds_lane, lds_pln, lds_dsk, lds_box, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
     int32_t path;            // RG_PATH_* forced by rg_debug_set_path, or RG_PATH_AUTO
     // frame
     uint32_t width, height;
@@ -129,12 +144,31 @@ struct RgKernelArgs {
     // outputs
     uint32_t *rgba;          // packed RGBA8, out_rows * width
     float *rgb;              // nullable, out_rows * width * 3
+    const uint32_t *tile_perm;     // nullable: dequeue order of the 8x8 tiles (expensive first)
     unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=~error key [16+16q]=tile queue heads (RG_COUNTER_WORDS words)
 };
+
+#ifndef RG_LB
+#define RG_LB 3                   // lights per shadow batch on the light path (its LB template parameter)
+#endif
+#ifndef RG_HEAVY_SCENE_BODIES
+#define RG_HEAVY_SCENE_BODIES 32  // bodies per ray at which the trace loop, not shading, dominates
+#endif
 
 #define RG_PATH_AUTO -1
 #define RG_PATH_LIGHT 0   // 2 waves/SIMD, batched shadow rays, exact f64 tests only
 #define RG_PATH_HEAVY 1   // 4 waves/SIMD, one ray per lane, f32 pre-filter + exact f64 tests
+
+// Kernel path of a launch (the launcher and the host's tile-order policy agree on it).
+__host__ __device__ __forceinline__ bool rg_heavy_path(const RgKernelArgs &a) {
+    bool heavy = a.n_sph + a.n_pln + a.n_dsk + a.n_box >= RG_HEAVY_SCENE_BODIES;
+#if defined(RG_FORCE_WPS)
+    heavy = RG_FORCE_WPS != 2;
+#endif
+    if (a.path != RG_PATH_AUTO) heavy = a.path == RG_PATH_HEAVY;
+    if (a.n_lights > RG_LB) heavy = true;  // the light path shades all lights in ONE batch
+    return heavy;
+}
 
 #define RG_COUNTER_WORDS (16 + 16 * 16)  // stats + 16 queue heads, 128 B apart
 

@@ -152,7 +152,10 @@ struct SphScalar {
     const RG_CONST RgDsk *dk;
     const RG_CONST RgBox *bx;
     const RG_CONST RgBvhNode *nd;
+    const RgBvhLane *ln;   // per-lane (divergent) index: plain global loads
     __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
+    __device__ __forceinline__ RgBvhLane getl(int i) const { return ln[i]; }
+    __device__ __forceinline__ RgSph getv(int i) const { return ((const RgSph *)s)[i]; }
     __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
     __device__ __forceinline__ RgDsk getd(int i) const { return dk[i]; }
     __device__ __forceinline__ RgBox getb(int i) const { return bx[i]; }
@@ -170,7 +173,10 @@ struct SphLds {
     const RgDsk *dk;
     const RgBox *bx;
     const RgBvhNode *nd;
+    const RgBvhLane *ln;
     __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
+    __device__ __forceinline__ RgBvhLane getl(int i) const { return ln[i]; }
+    __device__ __forceinline__ RgSph getv(int i) const { return s[i]; }
     __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
     __device__ __forceinline__ RgDsk getd(int i) const { return dk[i]; }
     __device__ __forceinline__ RgBox getb(int i) const { return bx[i]; }
@@ -552,6 +558,54 @@ __device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &sr
     RG_STAT(12, RG_CLOCK() - t_in);
 }
 
+// Per-lane traversal of the threaded binary layout (RgBvhLane): every lane
+// walks its own path (no stack: first child = next node, `miss` skips a
+// subtree), so an incoherent wave costs its slowest lane's path instead of
+// the union of all lanes' paths.  Same boxes, same bounds, same leaf tests
+// (f32 pre-filter, then the exact f64 test) as bvh_spheres.
+#ifndef RG_BVH_LANE_KINDS
+#define RG_BVH_LANE_KINDS 0   // bit 1: closest-hit queries, bit 2: shadow queries walk per lane
+#endif
+template <int KIND, class Src>
+__device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, V3 o, V3 d, double ld, double t0s,
+                                         Closest &c, bool &occl, bool &need) {
+    const V3 ob = t0s > 0.0 ? add(o, scl(d, t0s)) : o;
+    const RayB rb = rg_make_rayb(ob.x, ob.y, ob.z, d.x, d.y, d.z);
+    const RayF rf = make_rayf(o, d);
+    const float tld = KIND == 2 ? bvh_bound(ld - t0s) : 0.0f;
+    int node = 0;
+    for (;;) {
+        const bool act = need && node >= 0;
+        if (!__any(act)) break;
+        if (act) {
+            const RgBvhLane N = src.getl(node);
+            if (N.sph < 0) {
+                const float tb = KIND == 2 ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
+                node = rg_box_hit(N.a, N.b, rb, tb) ? node + 1 : N.miss;
+            } else {
+                const int j = N.sph;
+                const RgSphF f = {N.a[0], N.a[1], N.a[2], N.b[0]};
+                const RgSphF2 f2 = {N.b[1], 0.0f, 0.0f, 0.0f};
+                if (filter_general(f, f2, rf)) {
+                    const RgSph sp = src.getv(j);
+                    const double hx = sp.cx - o.x, hy = sp.cy - o.y, hz = sp.cz - o.z;
+                    const double adj = (hx * d.x + hy * d.y) + hz * d.z;
+                    const double opp = ((hx * hx + hy * hy) + hz * hz) - adj * adj;
+                    double t;
+                    if (!(opp > sp.r2) && sphere_tail(sp.r2, opp, adj, t)) {
+                        if (KIND == 2) {
+                            if (!(t > ld)) { occl = true; need = false; }
+                        } else {
+                            closest_add(c, t, a.sph_id[j]);
+                        }
+                    }
+                }
+                node = N.miss;
+            }
+        }
+    }
+}
+
 template <bool F32F, bool BVH, class Src>
 __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
     if constexpr (!BVH) sph_primary<F32F>(a, src, d, c);
@@ -670,8 +724,13 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
             RG_STAT(13, RG_CLOCK() - t0);
         }
         if (ok) {
-            if (shadow) bvh_spheres<2>(a, src, o, d, ld, t0s, c, occl, need);
-            else bvh_spheres<1>(a, src, o, d, ld, t0s, c, occl, need);
+            if (shadow) {
+                if constexpr (RG_BVH_LANE_KINDS & 4) bvh_lane<2>(a, src, o, d, ld, t0s, c, occl, need);
+                else bvh_spheres<2>(a, src, o, d, ld, t0s, c, occl, need);
+            } else {
+                if constexpr (RG_BVH_LANE_KINDS & 2) bvh_lane<1>(a, src, o, d, ld, t0s, c, occl, need);
+                else bvh_spheres<1>(a, src, o, d, ld, t0s, c, occl, need);
+            }
         }
     }
 }
@@ -683,9 +742,7 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
 // once and only adj/opp/compare are per light, so a 3-light batch costs
 // 8 + 3*8 FP64 ops per sphere instead of 3*16, with bit-identical per-ray
 // arithmetic.  Bit l of `occl` = light l of the batch is occluded.
-#ifndef RG_LB
-#define RG_LB 3            // lights per shadow batch for light scenes (LB template parameter)
-#endif
+// RG_LB (lights per shadow batch on the light path) lives in rg_device.h
 #ifndef RG_SHADOW_GROUP
 #define RG_SHADOW_GROUP 2  // spheres per miss-test group in the shadow pass
 #endif
@@ -1000,7 +1057,10 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         stage16(smem + (size_t)a.n_sph * sizeof(RgSphF), a.sphf2, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF2));
         stage16(smem + a.lds_sph, a.sph, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSph));
         stage16(smem + a.lds_cc, a.sph_cc, a.lds_nodes - a.lds_cc);
-        if constexpr (BVH) stage16(smem + a.lds_nodes, a.nodes, (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode));
+        if constexpr (BVH) {
+            stage16(smem + a.lds_nodes, a.nodes, (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode));
+            stage16(smem + a.lds_lane, a.lane_nodes, (uint32_t)a.n_lane_nodes * (uint32_t)sizeof(RgBvhLane));
+        }
         stage16(smem + a.lds_pln, a.pln, (uint32_t)a.n_pln * (uint32_t)sizeof(RgPln));
         stage16(smem + a.lds_dsk, a.dsk, (uint32_t)a.n_dsk * (uint32_t)sizeof(RgDsk));
         stage16(smem + a.lds_box, a.box, a.lds_bodies - a.lds_box);
@@ -1012,6 +1072,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         src.dk = reinterpret_cast<const RgDsk *>(smem + a.lds_dsk);
         src.bx = reinterpret_cast<const RgBox *>(smem + a.lds_box);
         src.nd = reinterpret_cast<const RgBvhNode *>(smem + a.lds_nodes);
+        src.ln = reinterpret_cast<const RgBvhLane *>(smem + a.lds_lane);
     } else {
         src.s = rg_cptr(a.sph);
         src.cc = rg_cptr(a.sph_cc);
@@ -1021,6 +1082,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         src.dk = rg_cptr(a.dsk);
         src.bx = rg_cptr(a.box);
         src.nd = rg_cptr(a.nodes);
+        src.ln = a.lane_nodes;
     }
     if constexpr (LCOLD) {
         stage16(smem + a.lds_bodies, a.bodies, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgBodyDev));
@@ -1083,7 +1145,12 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             ++qtried;
         }
         if (tile == 0xFFFFFFFFu) break;
+        if (a.tile_perm) tile = a.tile_perm[tile];  // scheduling order only; every tile is rendered once
         const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+#ifdef RG_TILE_TIMES
+        const unsigned long long t_tile = wall_clock64();  // diagnostic: per-tile time into rgb[tile] (us),
+        uint32_t tile_iters = 0;                           // wave iterations into rgb[ntiles + tile]
+#endif
         const uint32_t x = tx * 8u + (uint32_t)(lane & 7);
         const uint32_t orow = ty * 8u + (uint32_t)(lane >> 3);
         bool alive = x < a.width && orow < a.out_rows;
@@ -1091,7 +1158,9 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         const size_t oidx = (size_t)orow * a.width + x;
         if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
             a.rgba[oidx] = 0u;
+#ifndef RG_TILE_TIMES
             if (a.rgb) { a.rgb[3 * oidx] = 0.0f; a.rgb[3 * oidx + 1] = 0.0f; a.rgb[3 * oidx + 2] = 0.0f; }
+#endif
             alive = false;
         }
         const uint32_t pixel = y * a.width + x;
@@ -1321,7 +1390,9 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                         if (sp == 0) {
                             a.rgba[oidx] = f32_to_u8(ret.r * 255.0f) | (f32_to_u8(ret.g * 255.0f) << 8) |
                                            (f32_to_u8(ret.b * 255.0f) << 16) | 0xFF000000u;
+#ifndef RG_TILE_TIMES
                             if (a.rgb) { a.rgb[3 * oidx] = ret.r; a.rgb[3 * oidx + 1] = ret.g; a.rgb[3 * oidx + 2] = ret.b; }
+#endif
                             mode = MODE_DONE;
                             break;
                         }
@@ -1349,6 +1420,9 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             }
             const bool live = mode != MODE_DONE;
             if (!__any(live)) break;
+#ifdef RG_TILE_TIMES
+            ++tile_iters;
+#endif
             if (live) {
                 closest_init(c);
                 occl = 0u;
@@ -1382,6 +1456,12 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             }
             have_result = live;
         }
+#ifdef RG_TILE_TIMES
+        if (lane == 0 && a.rgb) {
+            a.rgb[tile] = (float)(wall_clock64() - t_tile) * 0.01f;  // 100 MHz clock
+            a.rgb[ntiles + tile] = (float)tile_iters;
+        }
+#endif
     }
 
     RG_STAT(14, RG_CLOCK() - t_kernel);
@@ -1415,7 +1495,7 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
     bool occl = false;
     if (alive) {
         SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc), rg_cptr(a.sphf), rg_cptr(a.sphf2),
-                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes)};
+                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes), a.lane_nodes};
         if (a.n_nodes > 0) trace_query<true, true>(a, src, r, false, 0.0, c, occl);
         else if (a.path == RG_PATH_HEAVY) trace_query<true, false>(a, src, r, false, 0.0, c, occl);
         else trace_query<false, false>(a, src, r, false, 0.0, c, occl);
@@ -1423,6 +1503,160 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
         dist[i] = c.id >= 0 ? c.t : 0.0;
         body[i] = c.id;
     }
+}
+
+// ---------------------------------------------------------------- tile ordering
+// A frame's makespan is max(average work per wave, slowest tile) only if the
+// slowest tiles START early; in raster order an expensive band (refractive or
+// reflective surfaces: ray trees of up to 2^depth rays per pixel) can start
+// late and end the frame alone.  A probe traces 8 primary rays per 8x8 tile
+// (NOT counted as rays of the frame), weights each by the material it hits,
+// and a counting sort (wave-aggregated histogram, scan, scatter) orders the
+// tile queue by descending weight (longest-processing-time-first).  This changes only the
+// order in which tiles are dequeued: every pixel is still computed once, by
+// the same code, so the output is identical.
+#define RG_PROBE_SAMPLES 8   // per tile: 4 corners + 4 inner points; 8 tiles per wave
+#define RG_ORDER_BUCKETS 16
+
+__device__ __forceinline__ uint32_t probe_weight(const RgKernelArgs &a, const Closest &c) {
+    if (c.id < 0) return 1u;                                        // sky: one ray
+    const int s = a.mats[c.id].surface;
+    const uint32_t diffuse = 2u + (uint32_t)a.n_lights;              // primary + shadow rays
+    if (a.max_depth <= 1) return diffuse;
+    if (s == RG_SURFACE_REFRACTIVE) return 8u * diffuse;            // a ray tree below the hit
+    if (s == RG_SURFACE_REFLECTING) return 3u * diffuse;            // a reflection chain
+    return diffuse;
+}
+// bucket 0 = heaviest; a tile's weight is the sum of its 8 samples
+__device__ __forceinline__ uint32_t order_bucket(uint32_t w) {
+    return (RG_ORDER_BUCKETS - 1u) - min(w >> 4, RG_ORDER_BUCKETS - 1u);
+}
+
+#define RG_ORDER_CHUNK 1024  // tiles per counting/scatter chunk (one wave each)
+
+// 1) probe: 8 consecutive lanes per tile; writes the tile's bucket
+template <bool BVH>
+__global__ __launch_bounds__(256) void rg_tile_probe_kernel(RgKernelArgs a, uint32_t *bucket_of, uint32_t ntiles) {
+    const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t tile = gid / RG_PROBE_SAMPLES, smp = gid % RG_PROBE_SAMPLES;
+    const uint32_t tiles_x = (a.width + 7u) / 8u;
+    bool alive = tile < ntiles;
+    const uint32_t ty = alive ? tile / tiles_x : 0u, tx = alive ? tile - ty * tiles_x : 0u;
+    const uint32_t ox = (smp & 3u) == 0u ? 0u : (smp & 3u) == 1u ? 7u : (smp & 3u) == 2u ? 2u : 5u;
+    const uint32_t oy = smp < 4u ? ((smp & 1u) ? 7u : 0u) : ((smp & 1u) ? 5u : 2u);
+    const uint32_t x = min(tx * 8u + ox, a.width - 1u);
+    const uint32_t orow = min(ty * 8u + oy, a.out_rows - 1u);
+    const uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
+    uint32_t w = 0u;
+    if (alive && y != 0xFFFFFFFFu) {
+        Closest c;
+        closest_init(c);
+        SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc), rg_cptr(a.sphf), rg_cptr(a.sphf2),
+                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes), a.lane_nodes};
+        const double sx = ((((double)x + 0.5) / (double)a.width) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
+        const double sy = (1.0 - (((double)y + 0.5) / (double)a.height) * 2.0) * a.fov_adjustment;
+        trace_primary<true, BVH>(a, src, normalize(v3(sx, sy, -1.0)), c);
+        w = probe_weight(a, c);
+    }
+    w += (uint32_t)__shfl_xor((int)w, 1, 64);
+    w += (uint32_t)__shfl_xor((int)w, 2, 64);
+    w += (uint32_t)__shfl_xor((int)w, 4, 64);
+    if (alive && smp == 0u) bucket_of[tile] = order_bucket(w);
+}
+
+// 2) per-chunk bucket histograms (one wave per chunk; no global atomics)
+__global__ __launch_bounds__(64) void rg_tile_count_kernel(const uint32_t *bucket_of, uint32_t *chunk_hist,
+                                                           uint32_t ntiles) {
+    __shared__ uint32_t hist[RG_ORDER_BUCKETS];
+    const uint32_t lane = threadIdx.x;
+    if (lane < RG_ORDER_BUCKETS) hist[lane] = 0u;
+    __syncthreads();
+    const uint32_t c0 = blockIdx.x * RG_ORDER_CHUNK, c1 = min(c0 + RG_ORDER_CHUNK, ntiles);
+    for (uint32_t t = c0 + lane; t < c1; t += 64u) atomicAdd(&hist[bucket_of[t]], 1u);
+    __syncthreads();
+    if (lane < RG_ORDER_BUCKETS) chunk_hist[lane * gridDim.x + blockIdx.x] = hist[lane];  // bucket-major: the scan order
+}
+
+// 3) exclusive scan in (bucket, chunk) order -> each chunk's first slot per bucket
+//    (one block: per-thread serial sums over contiguous ranges, shuffle scans)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = (int)(threadIdx.x & 63u);
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+__global__ __launch_bounds__(1024) void rg_tile_scan_kernel(uint32_t *chunk_hist, uint32_t nchunks) {
+    __shared__ uint32_t wave_tot[16];
+    const uint32_t n = nchunks * RG_ORDER_BUCKETS;
+    const uint32_t per = (n + 1023u) / 1024u;
+    const uint32_t i0 = threadIdx.x * per, i1 = min(i0 + per, n);
+    // chunk_hist is bucket-major (element k = bucket k / nchunks, chunk k % nchunks)
+    auto at = [&](uint32_t k) -> uint32_t & { return chunk_hist[k]; };
+    uint32_t sum = 0u;
+    for (uint32_t k = i0; k < i1; ++k) sum += at(k);
+    const uint32_t incl = wave_incl_scan(sum);
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 63u) wave_tot[w] = incl;
+    __syncthreads();
+    if (w == 0) {
+        const uint32_t t = (threadIdx.x < 16u) ? wave_tot[threadIdx.x] : 0u;
+        const uint32_t ti = wave_incl_scan(t);
+        if (threadIdx.x < 16u) wave_tot[threadIdx.x] = ti - t;  // exclusive wave offsets
+    }
+    __syncthreads();
+    uint32_t run = wave_tot[w] + incl - sum;
+    for (uint32_t k = i0; k < i1; ++k) { const uint32_t v = at(k); at(k) = run; run += v; }
+}
+
+// 4) stable scatter: one wave walks its chunk in raster order
+__global__ __launch_bounds__(64) void rg_tile_scatter_kernel(const uint32_t *bucket_of, const uint32_t *chunk_base,
+                                                             uint32_t *perm, uint32_t ntiles) {
+    __shared__ uint32_t cur[RG_ORDER_BUCKETS];
+    const uint32_t lane = threadIdx.x;
+    if (lane < RG_ORDER_BUCKETS) cur[lane] = chunk_base[lane * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const uint32_t c0 = blockIdx.x * RG_ORDER_CHUNK, c1 = min(c0 + RG_ORDER_CHUNK, ntiles);
+    for (uint32_t t0 = c0; t0 < c1; t0 += 64u) {
+        const uint32_t t = t0 + lane;
+        const bool act = t < c1;
+        const uint32_t b = act ? bucket_of[t] : 0u;
+        unsigned long long todo = __ballot(act);
+        while (todo) {  // one pass per distinct bucket in this group of 64 tiles
+            const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+            const uint32_t k = (uint32_t)__shfl((int)b, (int)leader, 64);
+            const unsigned long long grp = __ballot(act && b == k);
+            if (act && b == k) perm[cur[k] + (uint32_t)__builtin_popcountll(grp & ((1ull << lane) - 1ull))] = t;
+            __syncthreads();
+            if (lane == leader) cur[k] += (uint32_t)__builtin_popcountll(grp);
+            __syncthreads();
+            todo &= ~grp;
+        }
+    }
+}
+
+// scratch: [bucket_of ntiles | chunk_hist 64 * nchunks (bucket-major)]
+extern "C" size_t rg_tile_order_scratch_words(uint32_t ntiles) {
+    const size_t nchunks = (ntiles + RG_ORDER_CHUNK - 1u) / RG_ORDER_CHUNK;
+    return (size_t)ntiles + nchunks * RG_ORDER_BUCKETS;
+}
+
+extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scratch, uint32_t *perm, hipStream_t stream) {
+    const uint32_t ntiles = ((a->width + 7u) / 8u) * ((a->out_rows + 7u) / 8u);
+    const uint32_t nchunks = (ntiles + RG_ORDER_CHUNK - 1u) / RG_ORDER_CHUNK;
+    uint32_t *bucket_of = scratch, *chunk_hist = scratch + ntiles;
+    const uint32_t lanes = ntiles * RG_PROBE_SAMPLES;
+    if (a->n_nodes > 0)
+        hipLaunchKernelGGL(rg_tile_probe_kernel<true>, dim3((lanes + 255u) / 256u), dim3(256), 0, stream, *a, bucket_of,
+                           ntiles);
+    else
+        hipLaunchKernelGGL(rg_tile_probe_kernel<false>, dim3((lanes + 255u) / 256u), dim3(256), 0, stream, *a,
+                           bucket_of, ntiles);
+    hipLaunchKernelGGL(rg_tile_count_kernel, dim3(nchunks), dim3(64), 0, stream, bucket_of, chunk_hist, ntiles);
+    hipLaunchKernelGGL(rg_tile_scan_kernel, dim3(1), dim3(1024), 0, stream, chunk_hist, nchunks);
+    hipLaunchKernelGGL(rg_tile_scatter_kernel, dim3(nchunks), dim3(64), 0, stream, bucket_of, chunk_hist, perm, ntiles);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- launchers
@@ -1466,9 +1700,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
 #ifndef RG_HEAVY_F32_FILTER
 #define RG_HEAVY_F32_FILTER true  // heavy path: f32 pre-filter in front of the exact sphere tests
 #endif
-#ifndef RG_HEAVY_SCENE_BODIES
-#define RG_HEAVY_SCENE_BODIES 32         // bodies per ray at which the trace loop, not shading, dominates
-#endif
+// RG_HEAVY_SCENE_BODIES and the path decision (rg_heavy_path) live in rg_device.h
 
 template <int MAXD, int WPS, int LB, bool F32F, bool BVH>
 static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream) {
@@ -1491,12 +1723,7 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
     // fatter iterations (RG_LB shadow rays per pass) at 2 waves/SIMD.  Heavy
     // scenes: the body loop dominates and waves mix ray kinds -> one ray per
     // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
-    bool heavy = a->n_sph + a->n_pln + a->n_dsk + a->n_box >= RG_HEAVY_SCENE_BODIES;
-#if defined(RG_FORCE_WPS)
-    heavy = RG_FORCE_WPS != 2;
-#endif
-    if (a->path != RG_PATH_AUTO) heavy = a->path == RG_PATH_HEAVY;
-    if (a->n_lights > RG_LB) heavy = true;  // the light path shades all lights in ONE batch
+    const bool heavy = rg_heavy_path(*a);
     if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false>(a, stream);
     if (a->n_nodes > 0) return launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true>(a, stream);
     return launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false>(a, stream);

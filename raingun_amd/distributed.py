@@ -55,13 +55,30 @@ def assemble(gathered, height: int, world: int, tile_rows: int = TILE_ROWS):
     else:
         import torch
 
-        g = torch.stack(list(gathered)) if isinstance(gathered, (list, tuple)) else gathered
+        if isinstance(gathered, (list, tuple)):
+            base = gathered[0]._base if gathered[0]._base is not None else None
+            # views of one (world, slot, W, C) tensor (gather_buffers()): no stacking copy
+            if (base is not None and base.dim() == 4 and base.shape[0] == len(gathered) and
+                    all(t._base is base for t in gathered) and gathered[0].data_ptr() == base.data_ptr()):
+                g = base
+            else:
+                g = torch.stack(list(gathered))
+        else:
+            g = gathered
     tpr = tiles_per_rank(height, world, tile_rows)
     w, c = g.shape[-2], g.shape[-1]
     g = g.reshape(world, tpr, tile_rows, w, c)
     # tile j*world + r lives in g[r, j]
     g = g.transpose(1, 0, 2, 3, 4) if is_np else g.transpose(0, 1)
     return g.reshape(world * tpr * tile_rows, w, c)[:height]
+
+
+def gather_buffers(part, world: int):
+    """Rank 0's receive buffers for render_frame: `world` views of ONE
+    (world, slot_rows, W, C) tensor, so assemble() re-interleaves them with a
+    single copy."""
+    big = part.new_empty((world,) + tuple(part.shape))
+    return list(big.unbind(0))
 
 
 def render_frame(render_tiles: Callable[[object], object], height: int, rank: int, world: int,

@@ -269,6 +269,10 @@ class DeviceScene:
         """Use (default) or bypass the sphere BVH (include/raingun_debug.h)."""
         _abi.check(_abi.lib().rg_debug_set_bvh(self.handle, 1 if enable else 0))
 
+    def set_tile_order(self, mode) -> None:
+        """Tile scheduling: True/1 probe-ordered, False/0 raster, -1 auto (include/raingun_debug.h)."""
+        _abi.check(_abi.lib().rg_debug_set_tile_order(self.handle, int(mode)))
+
     def bvh_info(self) -> _abi.rg_bvh_info:
         info = _abi.rg_bvh_info()
         _abi.check(_abi.lib().rg_debug_bvh_info(self.handle, C.byref(info)))

@@ -113,6 +113,34 @@ static Hit bvh_trace(const Scene &S, const double o[3], const double d[3], doubl
     return h;
 }
 
+// per-lane walk of the threaded layout (RgBvhLane), as bvh_lane in the kernel
+static long g_lane_steps = 0;
+static Hit lane_trace(const Scene &S, const double o[3], const double d[3], double ld, double t0s, bool &any) {
+    const double ob[3] = {o[0] + d[0] * t0s, o[1] + d[1] * t0s, o[2] + d[2] * t0s};
+    const RayB rb = t0s > 0.0 ? rg_make_rayb(ob[0], ob[1], ob[2], d[0], d[1], d[2])
+                              : rg_make_rayb(o[0], o[1], o[2], d[0], d[1], d[2]);
+    Hit h{0.0, -1};
+    any = false;
+    const bool shadow = ld >= 0.0;
+    int node = 0;
+    while (node >= 0) {
+        ++g_lane_steps;
+        const RgBvhLane &N = S.bvh.lane[node];
+        if (N.sph < 0) {
+            const float tb = shadow ? bound(ld - t0s) : (h.id >= 0 ? bound(h.t - t0s) : HUGE_VALF);
+            node = rg_box_hit(N.a, N.b, rb, tb) ? node + 1 : N.miss;
+        } else {
+            double t;
+            if (sphere_exact(&S.sp_bvh[4 * N.sph], o, d, t)) {
+                if (shadow) { if (!(t > ld)) { any = true; return h; } }
+                else add(h, t, (int)S.bvh.order[N.sph]);
+            }
+            node = N.miss;
+        }
+    }
+    return h;
+}
+
 static uint64_t rng_state = 0x5EEDULL;
 static double urand() {  // SplitMix64 -> [0, 1)
     uint64_t z = (rng_state += 0x9E3779B97F4A7C15ULL);
@@ -157,6 +185,9 @@ int main(int argc, char **argv) {
                 }
             }
     for (int j = 0; j < n; ++j) if (seen[j] != 1) { std::fprintf(stderr, "leaf cover\n"); return 1; }
+    std::vector<int> lseen(n, 0);
+    for (const RgBvhLane &l : S.bvh.lane) if (l.sph >= 0) ++lseen[l.sph];
+    for (int j = 0; j < n; ++j) if (lseen[j] != 1) { std::fprintf(stderr, "lane leaf cover\n"); return 1; }
     }
 
     long rays = 0, fallback = 0, mism = 0, hits = 0, shadow_rays = 0, occluded = 0, shifted = 0, nosphere = 0;
@@ -172,6 +203,10 @@ int main(int argc, char **argv) {
         bool any = false;
         const Hit b = brute(S, o, d);
         const Hit v = cls == RG_BVH_NO_SPHERE ? Hit{0.0, -1} : bvh_trace(S, o, d, -1.0, t0s, any);
+        const Hit w = cls == RG_BVH_NO_SPHERE ? Hit{0.0, -1} : lane_trace(S, o, d, -1.0, t0s, any);
+        if (w.id != b.id || (b.id >= 0 && std::memcmp(&b.t, &w.t, 8) != 0)) {
+            if (++mism <= 5) std::fprintf(stderr, "lane closest mismatch brute %d bvh %d\n", b.id, w.id);
+        }
         if (b.id != v.id || (b.id >= 0 && std::memcmp(&b.t, &v.t, 8) != 0)) {
             if (++mism <= 5)
                 std::fprintf(stderr, "closest mismatch o=(%.17g %.17g %.17g) d=(%.17g %.17g %.17g) brute %d %.17g bvh %d %.17g\n",
@@ -184,6 +219,9 @@ int main(int argc, char **argv) {
             const bool ba = brute_any(S, o, d, ld);
             any = false;
             if (cls != RG_BVH_NO_SPHERE) bvh_trace(S, o, d, ld, t0s, any);
+            bool any2 = false;
+            if (cls != RG_BVH_NO_SPHERE) lane_trace(S, o, d, ld, t0s, any2);
+            if (ba != any2 && ++mism <= 5) std::fprintf(stderr, "lane shadow mismatch ld=%.17g\n", ld);
             occluded += ba;
             if (ba != any && ++mism <= 5) std::fprintf(stderr, "shadow mismatch ld=%.17g\n", ld);
         }
@@ -246,9 +284,10 @@ int main(int argc, char **argv) {
     std::printf("{\"spheres\": %d, \"nodes\": %zu, \"leaves\": %d, \"depth\": %d, \"margin\": %.6g, \"obound\": %.6g, "
                 "\"rays\": %ld, \"fallback\": %ld, \"hits\": %ld, \"shadow_rays\": %ld, \"occluded\": %ld, "
                 "\"shifted\": %ld, \"no_sphere\": %ld, "
-                "\"exact_tests_per_ray\": %.3f, \"nodes_per_ray\": %.3f, \"mismatches\": %ld}\n",
+                "\"exact_tests_per_ray\": %.3f, \"nodes_per_ray\": %.3f, \"lane_steps_per_ray\": %.3f, \"mismatches\": %ld}\n",
                 n, S.bvh.nodes.size(), S.bvh.leaves, S.bvh.depth, S.bvh.margin, (double)S.bvh.obound, rays, fallback,
                 hits, shadow_rays, occluded, shifted, nosphere, (double)g_tests / (double)(4 * (rays - fallback)),
-                (double)g_nodes / (double)(4 * (rays - fallback)), mism);
+                (double)g_nodes / (double)(4 * (rays - fallback)), (double)g_lane_steps / (double)(4 * (rays - fallback)),
+                mism);
     return mism ? 1 : 0;
 }

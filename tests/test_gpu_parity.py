@@ -253,3 +253,24 @@ def test_f32_prefilter_tangent_rays(oracle_lib, scale):
     own = (ob == targets) | (ob == -1)
     assert own.sum() > 1000
     assert 0.2 < (ob[own] == targets[own]).mean() < 0.8
+
+
+@pytest.mark.parametrize("scene_kind", ["synth200", "test1", "test3"])
+def test_tile_order_changes_nothing(oracle_lib, example_scenes, scene_kind):
+    """Probe-ordered tile scheduling (include/raingun_debug.h) only changes the
+    dequeue order: frame, f32 RGB and ray counts equal the raster-order render
+    and the CPU restatement, for whole frames and row tilings."""
+    scene = synthetic_scene(200, 2, 5) if scene_kind == "synth200" else example_scenes[scene_kind]
+    w, h = 320, 180
+    for order in (1, 0):
+        ds = DeviceScene(scene)
+        ds.set_tile_order(order)
+        st = _abi.rg_stats()
+        rgba, rgb = ds.render_tiles(w, h, want_rgb=True, stats=st)
+        part = ds.render_tiles(w, h, 16, 3, 2)
+        ds.close()
+        o_st, o_rgba, o_rgb, o_counts, _ = oracle_lib.render(SceneDesc(scene), w, h, want_rgb=True)
+        _, o_part, _, _, _ = oracle_lib.render(SceneDesc(scene), w, h, 16, 3, 2)
+        assert np.array_equal(rgba, o_rgba) and np.array_equal(part, o_part)
+        assert float(np.abs(rgb - o_rgb).max()) <= RGB_TOL
+        assert st.rays.as_dict() == o_counts
