@@ -490,9 +490,9 @@ __device__ __forceinline__ void leaf_query(const RgKernelArgs &a, const Src &src
 // distances shifted by t0s; the exact sphere tests use the ray as given.
 __device__ __forceinline__ float bvh_bound(double v) { return v <= 0.0 ? 0.0f : rg_f32_up(v); }
 
-template <int KIND, class Src>
+template <int KIND, bool GROW = false, class Src>
 __device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &src, V3 o, V3 d, double ld, double t0s,
-                                            Closest &c, bool &occl, bool &need) {
+                                            Closest &c, bool &occl, bool &need, float grow = 0.0f) {
     int *stack = rg_bvh_stack[threadIdx.x >> 6];
     const V3 ob = t0s > 0.0 ? add(o, scl(d, t0s)) : o;
     const RayB rb = rg_make_rayb(ob.x, ob.y, ob.z, d.x, d.y, d.z);
@@ -518,7 +518,7 @@ __device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &sr
         for (int k = 0; k < 4; ++k) {
             if (k < nch) {
                 float tn = 0.0f;
-                const bool h = need && rg_child_hit(N, k, rb, tb, tn);
+                const bool h = need && rg_child_hit<GROW>(N, k, rb, tb, tn, grow);
                 if (__any(h)) {
                     const int ch = wave_uniform(N.child[k]);
                     if (ch < 0) {
@@ -705,14 +705,15 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
     if constexpr (BVH) {  // spheres last: plane/disk/box hits already bound the search
         if (!__any(need)) return;
         double t0s = 0.0;
+        float grow = 0.0f;
         const int cls = (need && !c.nan) ? rg_bvh_classify(a.bvh_obound, a.bvh_rbound, a.bvh_margin, a.bvh_extent,
-                                                           o.x, o.y, o.z, d.x, d.y, d.z, t0s)
+                                                           o.x, o.y, o.z, d.x, d.y, d.z, t0s, grow)
                                          : RG_BVH_SCAN;
         const bool ok = need && cls == RG_BVH_TRAVERSE;
 #ifdef RG_BVH_STATS
         {
             RG_STAT(8, RG_LANES(need && cls == RG_BVH_SCAN));
-            RG_STAT(9, RG_LANES(need && cls == RG_BVH_TRAVERSE && t0s > 0.0));
+            RG_STAT(9, RG_LANES(need && cls == RG_BVH_TRAVERSE && grow > 0.0f));
             RG_STAT(10, RG_LANES(need && cls == RG_BVH_NO_SPHERE));
             RG_STAT(11, RG_LANES(need && c.nan));
         }
@@ -723,7 +724,8 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
             sph_query<F32F>(a, src, o, d, shadow, ld, c, occl, nd);
             RG_STAT(13, RG_CLOCK() - t0);
         }
-        if (ok) {
+        const bool grown = ok && grow > 0.0f;  // far rays: boxes grown in the slab test
+        if (ok && !grown) {
             if (shadow) {
                 if constexpr (RG_BVH_LANE_KINDS & 4) bvh_lane<2>(a, src, o, d, ld, t0s, c, occl, need);
                 else bvh_spheres<2>(a, src, o, d, ld, t0s, c, occl, need);
@@ -731,6 +733,10 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
                 if constexpr (RG_BVH_LANE_KINDS & 2) bvh_lane<1>(a, src, o, d, ld, t0s, c, occl, need);
                 else bvh_spheres<1>(a, src, o, d, ld, t0s, c, occl, need);
             }
+        }
+        if (grown) {
+            if (shadow) bvh_spheres<2, true>(a, src, o, d, ld, t0s, c, occl, need, grow);
+            else bvh_spheres<1, true>(a, src, o, d, ld, t0s, c, occl, need, grow);
         }
     }
 }

@@ -62,7 +62,8 @@ static long g_tests = 0, g_nodes = 0;
 // shadow: ld >= 0 -> any-hit within ld; ld < 0 -> closest hit
 static float bound(double v) { return v <= 0.0 ? 0.0f : rg_f32_up(v); }
 
-static Hit bvh_trace(const Scene &S, const double o[3], const double d[3], double ld, double t0s, bool &any) {
+static Hit bvh_trace(const Scene &S, const double o[3], const double d[3], double ld, double t0s, bool &any,
+                     float grow = 0.0f) {
     const double ob[3] = {o[0] + d[0] * t0s, o[1] + d[1] * t0s, o[2] + d[2] * t0s};
     const RayB rb = t0s > 0.0 ? rg_make_rayb(ob[0], ob[1], ob[2], d[0], d[1], d[2])
                               : rg_make_rayb(o[0], o[1], o[2], d[0], d[1], d[2]);
@@ -78,7 +79,7 @@ static Hit bvh_trace(const Scene &S, const double o[3], const double d[3], doubl
         float keys[4];
         for (int k = 0; k < N.nchild; ++k) {
             float tn;
-            if (!rg_child_hit(N, k, rb, tb, tn)) continue;
+            if (grow > 0.0f ? !rg_child_hit<true>(N, k, rb, tb, tn, grow) : !rg_child_hit(N, k, rb, tb, tn)) continue;
             if (N.child[k] < 0) {
                 const int v = ~N.child[k], first = v >> 3, count = (v & 7) + 1;
                 for (int j = first; j < first + count; ++j) {
@@ -190,20 +191,22 @@ int main(int argc, char **argv) {
     for (int j = 0; j < n; ++j) if (lseen[j] != 1) { std::fprintf(stderr, "lane leaf cover\n"); return 1; }
     }
 
-    long rays = 0, fallback = 0, mism = 0, hits = 0, shadow_rays = 0, occluded = 0, shifted = 0, nosphere = 0;
+    long rays = 0, fallback = 0, mism = 0, hits = 0, shadow_rays = 0, occluded = 0, shifted = 0, nosphere = 0, grown = 0;
     const double O = S.bvh.obound;
     auto check = [&](const double o[3], const double d[3]) {
         ++rays;
         double t0s = 0.0;
+        float grow = 0.0f;
         const int cls = rg_bvh_classify(S.bvh.obound, S.bvh.rbound, S.bvh.margin, S.bvh.extent, o[0], o[1], o[2], d[0],
-                                        d[1], d[2], t0s);
+                                        d[1], d[2], t0s, grow);
+        grown += grow > 0.0f;
         if (cls == RG_BVH_SCAN) { ++fallback; return; }
         shifted += t0s > 0.0;
         nosphere += cls == RG_BVH_NO_SPHERE;
         bool any = false;
         const Hit b = brute(S, o, d);
-        const Hit v = cls == RG_BVH_NO_SPHERE ? Hit{0.0, -1} : bvh_trace(S, o, d, -1.0, t0s, any);
-        const Hit w = cls == RG_BVH_NO_SPHERE ? Hit{0.0, -1} : lane_trace(S, o, d, -1.0, t0s, any);
+        const Hit v = cls == RG_BVH_NO_SPHERE ? Hit{0.0, -1} : bvh_trace(S, o, d, -1.0, t0s, any, grow);
+        const Hit w = (cls == RG_BVH_NO_SPHERE || grow > 0.0f) ? v : lane_trace(S, o, d, -1.0, t0s, any);
         if (w.id != b.id || (b.id >= 0 && std::memcmp(&b.t, &w.t, 8) != 0)) {
             if (++mism <= 5) std::fprintf(stderr, "lane closest mismatch brute %d bvh %d\n", b.id, w.id);
         }
@@ -218,9 +221,9 @@ int main(int argc, char **argv) {
             ++shadow_rays;
             const bool ba = brute_any(S, o, d, ld);
             any = false;
-            if (cls != RG_BVH_NO_SPHERE) bvh_trace(S, o, d, ld, t0s, any);
-            bool any2 = false;
-            if (cls != RG_BVH_NO_SPHERE) lane_trace(S, o, d, ld, t0s, any2);
+            if (cls != RG_BVH_NO_SPHERE) bvh_trace(S, o, d, ld, t0s, any, grow);
+            bool any2 = any;
+            if (cls != RG_BVH_NO_SPHERE && grow == 0.0f) lane_trace(S, o, d, ld, t0s, any2);
             if (ba != any2 && ++mism <= 5) std::fprintf(stderr, "lane shadow mismatch ld=%.17g\n", ld);
             occluded += ba;
             if (ba != any && ++mism <= 5) std::fprintf(stderr, "shadow mismatch ld=%.17g\n", ld);
@@ -269,7 +272,7 @@ int main(int argc, char **argv) {
     // 5. far origins (floor points seen at grazing angles): |o| from 1.5 O to 3e4 and beyond 1e7,
     //    directions towards a random sphere or random
     for (long i = 0; i < per_kind; ++i) {
-        const double R = O * (1.5 + urand() * (i % 3 == 0 ? 80.0 : 10.0)) * (i % 97 == 0 ? 1e5 : 1.0);
+        const double R = O * (1.5 + urand() * (i % 3 == 0 ? 80.0 : 10.0)) * (i % 13 == 0 ? 1e5 : (i % 7 == 0 ? 300.0 : 1.0));
         rand_dir(o);
         for (int k = 0; k < 3; ++k) o[k] *= R;
         if (i & 1) {
@@ -283,10 +286,10 @@ int main(int argc, char **argv) {
     }
     std::printf("{\"spheres\": %d, \"nodes\": %zu, \"leaves\": %d, \"depth\": %d, \"margin\": %.6g, \"obound\": %.6g, "
                 "\"rays\": %ld, \"fallback\": %ld, \"hits\": %ld, \"shadow_rays\": %ld, \"occluded\": %ld, "
-                "\"shifted\": %ld, \"no_sphere\": %ld, "
+                "\"shifted\": %ld, \"no_sphere\": %ld, \"grown\": %ld, "
                 "\"exact_tests_per_ray\": %.3f, \"nodes_per_ray\": %.3f, \"lane_steps_per_ray\": %.3f, \"mismatches\": %ld}\n",
                 n, S.bvh.nodes.size(), S.bvh.leaves, S.bvh.depth, S.bvh.margin, (double)S.bvh.obound, rays, fallback,
-                hits, shadow_rays, occluded, shifted, nosphere, (double)g_tests / (double)(4 * (rays - fallback)),
+                hits, shadow_rays, occluded, shifted, nosphere, grown, (double)g_tests / (double)(4 * (rays - fallback)),
                 (double)g_nodes / (double)(4 * (rays - fallback)), (double)g_lane_steps / (double)(4 * (rays - fallback)),
                 mism);
     return mism ? 1 : 0;
