@@ -28,10 +28,17 @@ typedef struct rg_bvh_info {
     int32_t depth;         /* levels */
     float margin;          /* box inflation, scene units */
     float origin_bound;    /* rays with |o_k| above this scan all spheres */
-    int32_t _pad;
+    int32_t lane_stack;    /* per-lane walk: worst-case stack entries per lane */
 } rg_bvh_info;
 rg_status rg_debug_set_bvh(rg_scene *scene, int32_t enable);
 rg_status rg_debug_bvh_info(const rg_scene *scene, rg_bvh_info *info);
+
+/* BVH walk per ray kind: rays at recursion depth >= min_depth (secondary rays
+ * and the shadow rays of their hits: incoherent) walk the tree per lane with a
+ * nearest-first stack; shallower rays walk it wave-coherently.  0 = every
+ * non-primary ray per lane, a large value = wave-coherent only, -1 = default
+ * (1).  Heavy path only; results are identical either way. */
+rg_status rg_debug_set_lane_depth(rg_scene *scene, int32_t min_depth);
 
 /* Tile scheduling: 1 = a primary-ray probe orders each frame's 8x8 tiles by
  * estimated cost, most expensive first (stable within a cost class);

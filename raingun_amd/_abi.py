@@ -109,7 +109,7 @@ class rg_tiling(C.Structure):
 
 class rg_bvh_info(C.Structure):  # include/raingun_debug.h
     _fields_ = [("built", C.c_int32), ("enabled", C.c_int32), ("nodes", C.c_int32), ("leaves", C.c_int32),
-                ("depth", C.c_int32), ("margin", C.c_float), ("origin_bound", C.c_float), ("_pad", C.c_int32)]
+                ("depth", C.c_int32), ("margin", C.c_float), ("origin_bound", C.c_float), ("lane_stack", C.c_int32)]
 
 
 TILE_CALLBACK = C.CFUNCTYPE(C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8), C.c_void_p)
@@ -131,7 +131,7 @@ EXPORTED_SYMBOLS = (
 )
 # include/raingun_debug.h
 DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
-                 "rg_debug_set_tile_order")
+                 "rg_debug_set_tile_order", "rg_debug_set_lane_depth")
 PATH_AUTO, PATH_LIGHT, PATH_HEAVY = -1, 0, 1
 
 
@@ -180,6 +180,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_bvh_info.argtypes = [C.c_void_p, P(rg_bvh_info)]
     lib.rg_debug_set_tile_order.restype = C.c_int32
     lib.rg_debug_set_tile_order.argtypes = [C.c_void_p, C.c_int32]
+    lib.rg_debug_set_lane_depth.restype = C.c_int32
+    lib.rg_debug_set_lane_depth.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_counters.restype = C.c_int32
     lib.rg_debug_counters.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.rg_trace.restype = C.c_int32

@@ -201,39 +201,20 @@ struct Collapser {
     }
 };
 
-// Threaded DFS layout: internal node, then its left subtree, then its right
-// subtree; every leaf sphere is its own node.  miss = index after the subtree.
-struct Threader {
-    const std::vector<BNode> &bn;
-    const std::vector<uint32_t> &idx;  // partitioned order: leaf ranges index the BVH-ordered tables
-    double margin;
-    std::vector<RgBvhLane> out;
-
-    void emit(int b) {
-        const BNode &n = bn[b];
-        if (n.count > 0) {
-            for (int j = n.first; j < n.first + n.count; ++j) {
-                RgBvhLane s;
-                for (int k = 0; k < 3; ++k) s.a[k] = s.b[k] = 0.0f;
-                s.sph = j;
-                s.miss = (int)out.size() + 1;
-                out.push_back(s);
-            }
-            return;
+// Per-lane nearest-first walk: visiting a node pushes all but one of its
+// internal children and descends into one, and a popped node is a sibling of an
+// ancestor, so the stack never exceeds max over root paths of sum (m - 1),
+// m = internal children of each node on the path.
+int lane_stack_need(const std::vector<RgBvhNode> &nodes, int i) {
+    const RgBvhNode &N = nodes[i];
+    int m = 0, below = 0;
+    for (int k = 0; k < N.nchild; ++k)
+        if (N.child[k] >= 0) {
+            ++m;
+            below = std::max(below, lane_stack_need(nodes, N.child[k]));
         }
-        const int me = (int)out.size();
-        RgBvhLane in;
-        for (int k = 0; k < 3; ++k) {
-            in.a[k] = f32_down(n.box.lo[k] - margin);
-            in.b[k] = f32_up(n.box.hi[k] + margin);
-        }
-        in.sph = -1;
-        out.push_back(in);
-        emit(n.left);
-        emit(n.right);
-        out[me].miss = (int)out.size();
-    }
-};
+    return m == 0 ? 0 : (m - 1) + below;
+}
 
 }  // namespace
 
@@ -272,12 +253,6 @@ bool rg_build_bvh(const double *sp, int n, RgBvhBuild &out) {
     c.out.reserve((size_t)n);
     c.emit(root, 0);
     out.nodes = std::move(c.out);
-    Threader th{b.bn, b.idx, margin, {}};
-    th.out.reserve(2 * (size_t)n);
-    th.emit(root);
-    for (RgBvhLane &l : th.out)
-        if (l.miss >= (int)th.out.size()) l.miss = -1;
-    out.lane = std::move(th.out);
     out.order = std::move(b.idx);
     out.obound = f32_down(O);
     out.margin = margin;
@@ -286,6 +261,7 @@ bool rg_build_bvh(const double *sp, int n, RgBvhBuild &out) {
     out.depth = c.depth;
     out.leaves = c.leaves;
     out.max_stack = 3 * c.depth;
+    out.lane_stack = lane_stack_need(out.nodes, 0);
     if (out.max_stack > 64) {
         out = RgBvhBuild();
         return false;

@@ -12,8 +12,6 @@
 
 struct RgBvhBuild {
     std::vector<RgBvhNode> nodes;   // nodes[0] is the root
-    std::vector<RgBvhLane> lane;    // threaded binary layout of the same tree (sphere leaves: filter
-                                    // fields left for the caller, which owns the f32 records)
     std::vector<uint32_t> order;    // BVH position -> index in the input sphere list
     float obound = 0.0f;            // origin bound |o_k| <= obound for which the boxes are conservative
     double margin = 0.0;            // box inflation (scene units)
@@ -22,6 +20,8 @@ struct RgBvhBuild {
     int depth = 0;                  // levels of the 4-wide tree
     int leaves = 0;
     int max_stack = 0;              // worst-case traversal stack entries (3 per level)
+    int lane_stack = 0;             // worst-case per-lane stack entries of the nearest-first walk:
+                                    // max over root paths of sum (internal children - 1)
 };
 
 // Build over spheres (center xyz, radius) given as n x 4 doubles.  Returns false

@@ -50,8 +50,11 @@ struct rg_scene {
     RgTexDev *texs = nullptr;
     RgBvhNode *nodes = nullptr;  // sphere BVH (sphere tables are in its leaf order)
     int32_t n_nodes = 0;
-    RgBvhLane *lane_nodes = nullptr;  // the same tree, threaded for per-lane traversal
-    int32_t n_lane_nodes = 0;
+    int32_t lane_stack = 0;      // per-lane walk stack entries the tree needs (0: per-lane walk unavailable)
+#ifndef RG_LANE_MIN_DEPTH
+#define RG_LANE_MIN_DEPTH 1
+#endif
+    int32_t lane_min_depth = RG_LANE_MIN_DEPTH;  // rays of this depth and deeper walk the BVH per lane
     bool bvh_enabled = true;
     float bvh_obound = 0.0f;
     double bvh_rbound = 0.0, bvh_margin = 0.0, bvh_extent = 0.0;
@@ -146,8 +149,6 @@ RgKernelArgs make_args(const rg_scene *s) {
     const bool bvh = s->bvh_enabled && s->n_nodes > 0;
     a.nodes = bvh ? s->nodes : nullptr;
     a.n_nodes = bvh ? s->n_nodes : 0;
-    a.lane_nodes = bvh ? s->lane_nodes : nullptr;
-    a.n_lane_nodes = bvh ? s->n_lane_nodes : 0;
     a.bvh_obound = s->bvh_obound;
     a.bvh_rbound = s->bvh_rbound;
     a.bvh_margin = s->bvh_margin;
@@ -162,13 +163,19 @@ RgKernelArgs make_args(const rg_scene *s) {
     a.n_bodies = s->n_bodies;
     a.n_lights = s->n_lights;
     a.n_textures = s->n_textures;
-    // LDS arena: [sphf | sphf2 | sph | cc (padded to 16 B) | nodes | pln | dsk | box (padded) | bodies | mats | lights | texs]
+    // per-lane BVH walk (heavy path only): stacks of lane_stack entries per thread at LDS offset 0
+    const bool lane = bvh && rg_heavy_path(a) && s->lane_stack > 0 && s->lane_min_depth < 1 << 20;
+    a.lane_stack = lane ? s->lane_stack : 0;
+    a.lane_min_depth = lane ? s->lane_min_depth : 1 << 30;
+    a.lds_lstack_bytes = (uint32_t)a.lane_stack * 256u * RG_HEAVY_WPS * 4u;
+    // LDS arena: [lane stacks | sphf | sphf2 | sph | cc (padded to 16 B) | nodes | pln | dsk | box (padded) |
+    //             bodies | mats | lights | texs]
     auto al16 = [](uint32_t v) { return (v + 15u) & ~15u; };
-    a.lds_sph = (uint32_t)s->n_sph * (uint32_t)(sizeof(RgSphF) + sizeof(RgSphF2));
+    a.lds_sphf = a.lds_lstack_bytes;
+    a.lds_sph = a.lds_sphf + (uint32_t)s->n_sph * (uint32_t)(sizeof(RgSphF) + sizeof(RgSphF2));
     a.lds_cc = a.lds_sph + (uint32_t)s->n_sph * (uint32_t)sizeof(RgSph);
     a.lds_nodes = al16(a.lds_cc + (uint32_t)s->n_sph * 8u);
-    a.lds_lane = a.lds_nodes + (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode);
-    a.lds_pln = a.lds_lane + (uint32_t)a.n_lane_nodes * (uint32_t)sizeof(RgBvhLane);
+    a.lds_pln = a.lds_nodes + (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode);
     a.lds_dsk = a.lds_pln + (uint32_t)s->n_pln * (uint32_t)sizeof(RgPln);
     a.lds_box = a.lds_dsk + (uint32_t)s->n_dsk * (uint32_t)sizeof(RgDsk);
     a.lds_bodies = al16(a.lds_box + (uint32_t)s->n_box * (uint32_t)sizeof(RgBox));
@@ -326,15 +333,6 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         permute(sphf2);
         permute(sph_cc);
         permute(sph_id);
-        for (RgBvhLane &l : bvh.lane) {  // sphere leaves carry their f32 pre-filter record
-            if (l.sph < 0) continue;
-            l.a[0] = sphf[l.sph].cx;
-            l.a[1] = sphf[l.sph].cy;
-            l.a[2] = sphf[l.sph].cz;
-            l.b[0] = sphf[l.sph].r2hi;
-            l.b[1] = sphf2[l.sph].cchi;
-            l.b[2] = 0.0f;
-        }
         s->bvh_obound = bvh.obound;
         s->bvh_rbound = bvh.rbound;
         s->bvh_margin = bvh.margin;
@@ -343,6 +341,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         s->bvh_info.nodes = (int32_t)bvh.nodes.size();
         s->bvh_info.leaves = bvh.leaves;
         s->bvh_info.depth = bvh.depth;
+        s->bvh_info.lane_stack = bvh.lane_stack;
         s->bvh_info.margin = (float)bvh.margin;
         s->bvh_info.origin_bound = bvh.obound;
     }
@@ -390,10 +389,11 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
     RG_UP(mats, mats);
     RG_UP(lights, lights);
     RG_UP(nodes, bvh.nodes);
-    RG_UP(lane_nodes, bvh.lane);
 #undef RG_UP
     s->n_nodes = (int32_t)bvh.nodes.size();
-    s->n_lane_nodes = (int32_t)bvh.lane.size();
+    // the stack entry keeps the node index in its low RG_LANE_NODE_BITS bits
+    s->lane_stack = (s->n_nodes <= (1 << RG_LANE_NODE_BITS) && bvh.lane_stack <= RG_LANE_STACK_MAX)
+                        ? std::max(bvh.lane_stack, 1) : 0;
     // textures: RGBA8 -> one u32 per texel (one 4-byte gather per lookup)
     std::vector<RgTexDev> texs(d->n_textures);
     for (uint32_t i = 0; st == RG_OK && i < d->n_textures; ++i) {
@@ -595,6 +595,12 @@ rg_status rg_debug_bvh_info(const rg_scene *s, rg_bvh_info *info) {
     if (!s || !info) return RG_ERR_INVALID_ARGUMENT;
     *info = s->bvh_info;
     info->enabled = s->bvh_enabled && s->n_nodes > 0;
+    return RG_OK;
+}
+
+rg_status rg_debug_set_lane_depth(rg_scene *s, int32_t min_depth) {
+    if (!s) return RG_ERR_INVALID_ARGUMENT;
+    s->lane_min_depth = min_depth < 0 ? RG_LANE_MIN_DEPTH : min_depth;
     return RG_OK;
 }
 

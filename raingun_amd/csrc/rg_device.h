@@ -55,17 +55,12 @@ struct alignas(16) RgBvhNode {
     int32_t pad[3];
 };
 
-// Threaded (stackless) binary BVH for per-lane traversal of incoherent rays:
-// nodes in DFS preorder, the first child of an internal node is the next
-// node, `miss` is where to go when a subtree is skipped (-1: done).  Internal
-// nodes hold the same conservative f32 box as the 4-wide tree (sph = -1);
-// leaf nodes are single spheres carrying their f32 pre-filter record.
-struct alignas(16) RgBvhLane {
-    float a[3];       // internal: box lo     | sphere: f32 centre (RgSphF cx, cy, cz)
-    float b[3];       // internal: box hi     | sphere: {r2hi, cchi, 0}
-    int32_t miss;     // next node when this one is missed / finished
-    int32_t sph;      // -1 internal; else the sphere's row in the (BVH-ordered) sphere tables
-};
+// Per-lane traversal (incoherent rays, rg_kernels.hip "bvh_lane") walks the
+// same 4-wide nodes with a per-lane stack in LDS.  Stack entry: the f32 bits
+// of the child's entry distance with the low RG_LANE_NODE_BITS cleared (a
+// lower bound, so pruning at pop is conservative) | the child's node index.
+#define RG_LANE_NODE_BITS 12
+#define RG_LANE_STACK_MAX 16      // entries per lane the LDS arena may hold
 
 struct RgBodyDev {         // per body, YAML order
     int32_t kind;
@@ -118,8 +113,8 @@ struct RgKernelArgs {
     // BVH over the spheres (n_nodes == 0: none; brute-force sphere loops)
     const RgBvhNode *nodes;
     int32_t n_nodes;
-    const RgBvhLane *lane_nodes;   // same spheres, threaded binary layout (per-lane traversal)
-    int32_t n_lane_nodes;
+    int32_t lane_stack;      // per-lane traversal stack entries (0: every lane walks wave-coherently)
+    int32_t lane_min_depth;  // rays at this recursion depth or deeper walk per lane (if lane_stack > 0)
     float bvh_obound;        // near-ray origin bound |o_k| (rg_bvh_ray.h)
     double bvh_rbound;       // far rays: half-size of the region holding every inflated sphere box
     double bvh_margin;       // box inflation m
@@ -131,8 +126,9 @@ struct RgKernelArgs {
     const RgTexDev *texs;
     int32_t n_bodies, n_lights, n_textures;
     // LDS arena (byte offsets; used by the LDS-staged kernel variants)
-    // [sphf | sphf2 | sph | cc | nodes | lane nodes | pln | dsk | box | bodies | mats | lights | texs] (byte offsets)
-    uint32_t lds_sph, lds_cc, lds_nodes, lds_lane, lds_pln, lds_dsk, lds_box, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
+    // [lane stacks | sphf | sphf2 | sph | cc | nodes | pln | dsk | box | bodies | mats | lights | texs] (byte offsets)
+    uint32_t lds_lstack_bytes;  // per-lane traversal stacks at offset 0: lane_stack x block threads x 4 B
+    uint32_t lds_sphf, lds_sph, lds_cc, lds_nodes, lds_pln, lds_dsk, lds_box, lds_bodies, lds_mats, lds_lights, lds_texs, lds_hot_bytes, lds_total_bytes;
     int32_t path;            // RG_PATH_* forced by rg_debug_set_path, or RG_PATH_AUTO
     // frame
     uint32_t width, height;
@@ -150,6 +146,9 @@ struct RgKernelArgs {
 
 #ifndef RG_LB
 #define RG_LB 3                   // lights per shadow batch on the light path (its LB template parameter)
+#endif
+#ifndef RG_HEAVY_WPS
+#define RG_HEAVY_WPS 3            // heavy path: waves per SIMD (block = 256 * WPS threads; 168 VGPRs)
 #endif
 #ifndef RG_HEAVY_SCENE_BODIES
 #define RG_HEAVY_SCENE_BODIES 32  // bodies per ray at which the trace loop, not shading, dominates

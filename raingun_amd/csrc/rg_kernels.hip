@@ -152,9 +152,7 @@ struct SphScalar {
     const RG_CONST RgDsk *dk;
     const RG_CONST RgBox *bx;
     const RG_CONST RgBvhNode *nd;
-    const RgBvhLane *ln;   // per-lane (divergent) index: plain global loads
     __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
-    __device__ __forceinline__ RgBvhLane getl(int i) const { return ln[i]; }
     __device__ __forceinline__ RgSph getv(int i) const { return ((const RgSph *)s)[i]; }
     __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
     __device__ __forceinline__ RgDsk getd(int i) const { return dk[i]; }
@@ -173,9 +171,7 @@ struct SphLds {
     const RgDsk *dk;
     const RgBox *bx;
     const RgBvhNode *nd;
-    const RgBvhLane *ln;
     __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
-    __device__ __forceinline__ RgBvhLane getl(int i) const { return ln[i]; }
     __device__ __forceinline__ RgSph getv(int i) const { return s[i]; }
     __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
     __device__ __forceinline__ RgDsk getd(int i) const { return dk[i]; }
@@ -558,52 +554,104 @@ __device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &sr
     RG_STAT(12, RG_CLOCK() - t_in);
 }
 
-// Per-lane traversal of the threaded binary layout (RgBvhLane): every lane
-// walks its own path (no stack: first child = next node, `miss` skips a
-// subtree), so an incoherent wave costs its slowest lane's path instead of
-// the union of all lanes' paths.  Same boxes, same bounds, same leaf tests
-// (f32 pre-filter, then the exact f64 test) as bvh_spheres.
-#ifndef RG_BVH_LANE_KINDS
-#define RG_BVH_LANE_KINDS 0   // bit 1: closest-hit queries, bit 2: shadow queries walk per lane
-#endif
+// Per-lane traversal for incoherent rays (secondary rays and the shadow rays
+// of their hits).  The wave-coherent walk above visits the UNION of its lanes'
+// paths; for 64 rays in 64 directions that is most of the tree, so every lane
+// here walks its own path: nearest-first over the same 4-wide nodes (per-lane
+// LDS gathers), the other hit children on a per-lane stack in LDS
+// (RG_LANE_NODE_BITS entry format, rg_device.h), each popped entry skipped when
+// its stored entry distance -- a lower bound -- already exceeds the current
+// bound, exactly as a fresh slab test against that bound would skip it.  Same
+// boxes, bounds and leaf tests (f32 pre-filter, then the exact f64 test) as
+// bvh_spheres, so the accepted set and every distance are identical.  The host
+// sizes the stack to the tree's worst case (rg_bvh.cpp lane_stack_need).
+extern __shared__ __attribute__((aligned(16))) unsigned char rg_dyn_smem[];
+
+__device__ __forceinline__ uint32_t lane_key(float tn, int node) {
+    return (__float_as_uint(tn) & ~((1u << RG_LANE_NODE_BITS) - 1u)) | (uint32_t)node;
+}
+__device__ __forceinline__ float lane_key_t(uint32_t e) {
+    return __uint_as_float(e & ~((1u << RG_LANE_NODE_BITS) - 1u));
+}
+__device__ __forceinline__ void cswap(uint32_t &x, uint32_t &y) {
+    const uint32_t lo = min(x, y), hi = max(x, y);
+    x = lo;
+    y = hi;
+}
+
 template <int KIND, class Src>
 __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, V3 o, V3 d, double ld, double t0s,
                                          Closest &c, bool &occl, bool &need) {
+    uint32_t *stk = reinterpret_cast<uint32_t *>(rg_dyn_smem) + threadIdx.x;  // entry e at stk[e * blockDim.x]
+    const uint32_t stride = blockDim.x;
+    const int cap = a.lane_stack;
+    const uint32_t mask = (1u << RG_LANE_NODE_BITS) - 1u;
     const V3 ob = t0s > 0.0 ? add(o, scl(d, t0s)) : o;
     const RayB rb = rg_make_rayb(ob.x, ob.y, ob.z, d.x, d.y, d.z);
     const RayF rf = make_rayf(o, d);
     const float tld = KIND == 2 ? bvh_bound(ld - t0s) : 0.0f;
-    int node = 0;
+    int node = 0, sp = 0;
+    RG_STAT(4, 1);
+    RG_STAT(7, RG_LANES(1));
+    [[maybe_unused]] const unsigned long long t_in = RG_CLOCK();
     for (;;) {
         const bool act = need && node >= 0;
         if (!__any(act)) break;
+        RG_STAT(5, 1);
         if (act) {
-            const RgBvhLane N = src.getl(node);
-            if (N.sph < 0) {
-                const float tb = KIND == 2 ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
-                node = rg_box_hit(N.a, N.b, rb, tb) ? node + 1 : N.miss;
-            } else {
-                const int j = N.sph;
-                const RgSphF f = {N.a[0], N.a[1], N.a[2], N.b[0]};
-                const RgSphF2 f2 = {N.b[1], 0.0f, 0.0f, 0.0f};
-                if (filter_general(f, f2, rf)) {
-                    const RgSph sp = src.getv(j);
-                    const double hx = sp.cx - o.x, hy = sp.cy - o.y, hz = sp.cz - o.z;
-                    const double adj = (hx * d.x + hy * d.y) + hz * d.z;
-                    const double opp = ((hx * hx + hy * hy) + hz * hz) - adj * adj;
-                    double t;
-                    if (!(opp > sp.r2) && sphere_tail(sp.r2, opp, adj, t)) {
-                        if (KIND == 2) {
-                            if (!(t > ld)) { occl = true; need = false; }
-                        } else {
-                            closest_add(c, t, a.sph_id[j]);
-                        }
+            const RgBvhNode N = src.getn(node);
+            const float tb = KIND == 2 ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
+            uint32_t e0 = ~0u, e1 = ~0u, e2 = ~0u, e3 = ~0u;
+            int l0 = 0, l1 = 0, l2 = 0, l3 = 0, nl = 0;  // hit leaf children, in child order
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float tn = 0.0f;
+                if (k < N.nchild && need && rg_child_hit(N, k, rb, tb, tn)) {
+                    const int ch = N.child[k];
+                    if (ch < 0) {
+                        if (nl == 0) l0 = ch;
+                        else if (nl == 1) l1 = ch;
+                        else if (nl == 2) l2 = ch;
+                        else l3 = ch;
+                        ++nl;
+                    } else {
+                        const uint32_t e = lane_key(tn, ch);
+                        if (k == 0) e0 = e;
+                        else if (k == 1) e1 = e;
+                        else if (k == 2) e2 = e;
+                        else e3 = e;
                     }
                 }
-                node = N.miss;
+            }
+            // leaves first (they tighten a closest-hit bound): ONE copy of the leaf
+            // test, looped max-over-lanes times, instead of one per child slot
+            while (nl > 0 && need) {
+                const int v = ~l0;
+                leaf_query(a, src, v >> 3, (v & 7) + 1, o, d, rf, KIND == 2, ld, c, occl, need);
+                l0 = l1; l1 = l2; l2 = l3;
+                --nl;
+            }
+            // ascending (entry distance, node); empty slots (~0) last
+            cswap(e0, e1); cswap(e2, e3); cswap(e0, e2); cswap(e1, e3); cswap(e1, e2);
+            if (e3 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e3;
+            if (e2 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e2;
+            if (e1 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e1;
+            const float tbn = KIND == 2 ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
+            if (e0 != ~0u && (KIND == 2 || !(lane_key_t(e0) > tbn))) {
+                node = (int)(e0 & mask);
+            } else {
+                node = -1;
+                while (sp > 0 && need) {
+                    const uint32_t e = stk[(uint32_t)(--sp) * stride];
+                    if (KIND == 2 || !(lane_key_t(e) > tbn)) {
+                        node = (int)(e & mask);
+                        break;
+                    }
+                }
             }
         }
     }
+    RG_STAT(12, RG_CLOCK() - t_in);
 }
 
 template <bool F32F, bool BVH, class Src>
@@ -654,7 +702,7 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
 // loops as soon as every lane that is still testing is a finished shadow ray.
 template <bool F32F, bool BVH, class Src>
 __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &src, const Ray &r, bool shadow, double ld,
-                                            Closest &c, bool &occl) {
+                                            Closest &c, bool &occl, bool lane_walk = false) {
     const V3 o = r.o, d = r.d;
     bool need = true;
     if constexpr (!BVH) {
@@ -725,14 +773,14 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
             RG_STAT(13, RG_CLOCK() - t0);
         }
         const bool grown = ok && grow > 0.0f;  // far rays: boxes grown in the slab test
-        if (ok && !grown) {
-            if (shadow) {
-                if constexpr (RG_BVH_LANE_KINDS & 4) bvh_lane<2>(a, src, o, d, ld, t0s, c, occl, need);
-                else bvh_spheres<2>(a, src, o, d, ld, t0s, c, occl, need);
-            } else {
-                if constexpr (RG_BVH_LANE_KINDS & 2) bvh_lane<1>(a, src, o, d, ld, t0s, c, occl, need);
-                else bvh_spheres<1>(a, src, o, d, ld, t0s, c, occl, need);
-            }
+        const bool per_lane = ok && !grown && lane_walk && a.lane_stack > 0;  // incoherent rays
+        if (per_lane) {
+            if (shadow) bvh_lane<2>(a, src, o, d, ld, t0s, c, occl, need);
+            else bvh_lane<1>(a, src, o, d, ld, t0s, c, occl, need);
+        }
+        if (ok && !grown && !per_lane) {
+            if (shadow) bvh_spheres<2>(a, src, o, d, ld, t0s, c, occl, need);
+            else bvh_spheres<1>(a, src, o, d, ld, t0s, c, occl, need);
         }
         if (grown) {
             if (shadow) bvh_spheres<2, true>(a, src, o, d, ld, t0s, c, occl, need, grow);
@@ -1059,26 +1107,24 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     typename std::conditional<LSPH, SphLds, SphScalar>::type src;
     Cold T;
     if constexpr (LSPH) {
-        stage16(smem, a.sphf, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF));
-        stage16(smem + (size_t)a.n_sph * sizeof(RgSphF), a.sphf2, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF2));
+        stage16(smem + a.lds_sphf, a.sphf, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF));
+        stage16(smem + a.lds_sphf + (size_t)a.n_sph * sizeof(RgSphF), a.sphf2, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF2));
         stage16(smem + a.lds_sph, a.sph, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSph));
         stage16(smem + a.lds_cc, a.sph_cc, a.lds_nodes - a.lds_cc);
         if constexpr (BVH) {
             stage16(smem + a.lds_nodes, a.nodes, (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode));
-            stage16(smem + a.lds_lane, a.lane_nodes, (uint32_t)a.n_lane_nodes * (uint32_t)sizeof(RgBvhLane));
         }
         stage16(smem + a.lds_pln, a.pln, (uint32_t)a.n_pln * (uint32_t)sizeof(RgPln));
         stage16(smem + a.lds_dsk, a.dsk, (uint32_t)a.n_dsk * (uint32_t)sizeof(RgDsk));
         stage16(smem + a.lds_box, a.box, a.lds_bodies - a.lds_box);
-        src.f = reinterpret_cast<const RgSphF *>(smem);
-        src.f2 = reinterpret_cast<const RgSphF2 *>(smem + (size_t)a.n_sph * sizeof(RgSphF));
+        src.f = reinterpret_cast<const RgSphF *>(smem + a.lds_sphf);
+        src.f2 = reinterpret_cast<const RgSphF2 *>(smem + a.lds_sphf + (size_t)a.n_sph * sizeof(RgSphF));
         src.s = reinterpret_cast<const RgSph *>(smem + a.lds_sph);
         src.cc = reinterpret_cast<const double *>(smem + a.lds_cc);
         src.pl = reinterpret_cast<const RgPln *>(smem + a.lds_pln);
         src.dk = reinterpret_cast<const RgDsk *>(smem + a.lds_dsk);
         src.bx = reinterpret_cast<const RgBox *>(smem + a.lds_box);
         src.nd = reinterpret_cast<const RgBvhNode *>(smem + a.lds_nodes);
-        src.ln = reinterpret_cast<const RgBvhLane *>(smem + a.lds_lane);
     } else {
         src.s = rg_cptr(a.sph);
         src.cc = rg_cptr(a.sph_cc);
@@ -1088,7 +1134,6 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         src.dk = rg_cptr(a.dsk);
         src.bx = rg_cptr(a.box);
         src.nd = rg_cptr(a.nodes);
-        src.ln = a.lane_nodes;
     }
     if constexpr (LCOLD) {
         stage16(smem + a.lds_bodies, a.bodies, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgBodyDev));
@@ -1156,6 +1201,14 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
 #ifdef RG_TILE_TIMES
         const unsigned long long t_tile = wall_clock64();  // diagnostic: per-tile time into rgb[tile] (us),
         uint32_t tile_iters = 0;                           // wave iterations into rgb[ntiles + tile]
+        unsigned long long t_query = 0;                    // time in the body/BVH queries into rgb[3 ntiles + tile]
+#ifdef RG_BVH_STATS  // with the BVH statistics: per-tile full-scan / traversal clocks and scan lanes
+        const unsigned long long st0_scan = rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][13];
+        const unsigned long long st0_trav = rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][12];
+        const unsigned long long st0_lanes = rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][8];
+        const unsigned long long st0_trv = rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][4];
+        const unsigned long long st0_steps = rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][5];
+#endif
 #endif
         const uint32_t x = tx * 8u + (uint32_t)(lane & 7);
         const uint32_t orow = ty * 8u + (uint32_t)(lane >> 3);
@@ -1433,6 +1486,9 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                 closest_init(c);
                 occl = 0u;
             }
+#ifdef RG_TILE_TIMES
+            const unsigned long long t_q0 = wall_clock64();
+#endif
             if constexpr (LB == 1) {
                 // one ray per lane, one pass: closest-hit and shadow lanes share the
                 // body loop (best when a wave mixes ray kinds over many bodies)
@@ -1441,7 +1497,8 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                     Ray r1;
                     r1.o = q.o;
                     r1.d = mode == MODE_SHADOW ? sb.d[0] : q.d;
-                    trace_query<F32F, BVH>(a, src, r1, mode == MODE_SHADOW, sb.ld[0], c, o1);
+                    const bool lane_walk = (mode == MODE_SHADOW ? hdepth : qdepth) >= (int)a.lane_min_depth;
+                    trace_query<F32F, BVH>(a, src, r1, mode == MODE_SHADOW, sb.ld[0], c, o1, lane_walk);
                     occl = o1 ? 1u : 0u;
                 }
             } else {
@@ -1460,12 +1517,24 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
 #endif
                 }
             }
+#ifdef RG_TILE_TIMES
+            t_query += wall_clock64() - t_q0;
+#endif
             have_result = live;
         }
 #ifdef RG_TILE_TIMES
         if (lane == 0 && a.rgb) {
             a.rgb[tile] = (float)(wall_clock64() - t_tile) * 0.01f;  // 100 MHz clock
             a.rgb[ntiles + tile] = (float)tile_iters;
+            a.rgb[2 * ntiles + tile] = (float)(t_tile & 0xFFFFFFull);  // start, 24-bit 100 MHz ticks (exact in f32)
+            a.rgb[3 * ntiles + tile] = (float)t_query * 0.01f;
+#ifdef RG_BVH_STATS
+            a.rgb[4 * ntiles + tile] = (float)(rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][13] - st0_scan) * 0.01f;
+            a.rgb[5 * ntiles + tile] = (float)(rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][12] - st0_trav) * 0.01f;
+            a.rgb[6 * ntiles + tile] = (float)(rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][8] - st0_lanes);
+            a.rgb[7 * ntiles + tile] = (float)(rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][4] - st0_trv);
+            a.rgb[8 * ntiles + tile] = (float)(rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][5] - st0_steps);
+#endif
         }
 #endif
     }
@@ -1501,8 +1570,8 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
     bool occl = false;
     if (alive) {
         SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc), rg_cptr(a.sphf), rg_cptr(a.sphf2),
-                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes), a.lane_nodes};
-        if (a.n_nodes > 0) trace_query<true, true>(a, src, r, false, 0.0, c, occl);
+                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes)};
+        if (a.n_nodes > 0) trace_query<true, true>(a, src, r, false, 0.0, c, occl, a.lane_min_depth <= 1);
         else if (a.path == RG_PATH_HEAVY) trace_query<true, false>(a, src, r, false, 0.0, c, occl);
         else trace_query<false, false>(a, src, r, false, 0.0, c, occl);
         if (c.nan && c.nhit >= 2) raise_error(a, i, RG_ERR_NAN_DISTANCE);
@@ -1558,7 +1627,7 @@ __global__ __launch_bounds__(256) void rg_tile_probe_kernel(RgKernelArgs a, uint
         Closest c;
         closest_init(c);
         SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc), rg_cptr(a.sphf), rg_cptr(a.sphf2),
-                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes), a.lane_nodes};
+                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes)};
         const double sx = ((((double)x + 0.5) / (double)a.width) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
         const double sy = (1.0 - (((double)y + 0.5) / (double)a.height) * 2.0) * a.fov_adjustment;
         trace_primary<true, BVH>(a, src, normalize(v3(sx, sy, -1.0)), c);
@@ -1700,9 +1769,6 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
 #ifndef RG_LDS_BUDGET
 #define RG_LDS_BUDGET (160 * 1024)       // one block per CU owns the CU's LDS
 #endif
-#ifndef RG_HEAVY_WPS
-#define RG_HEAVY_WPS 4            // heavy path: waves per SIMD (block = 256 * WPS threads)
-#endif
 #ifndef RG_HEAVY_F32_FILTER
 #define RG_HEAVY_F32_FILTER true  // heavy path: f32 pre-filter in front of the exact sphere tests
 #endif
@@ -1716,7 +1782,7 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream) {
         return launch_one<MAXD, true, true, WPS, LB, F32F, BVH>(a, a->lds_total_bytes, stream);
     if (a->n_sph > 0 && a->lds_hot_bytes <= budget)
         return launch_one<MAXD, true, false, WPS, LB, F32F, BVH>(a, a->lds_hot_bytes, stream);
-    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH>(a, 0, stream);
+    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH>(a, a->lds_lstack_bytes, stream);
 }
 
 #ifndef RG_LIGHT_WPS
@@ -1745,6 +1811,7 @@ extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStrea
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,
                                       int32_t *body, hipStream_t stream) {
     dim3 grid((n + 255) / 256);
-    hipLaunchKernelGGL(rg_trace_kernel, grid, dim3(256), 0, stream, *a, rays, n, dist, body);
+    const size_t lds = (size_t)a->lane_stack * 256u * 4u;  // per-lane walk stacks (stride = block size)
+    hipLaunchKernelGGL(rg_trace_kernel, grid, dim3(256), lds, stream, *a, rays, n, dist, body);
     return hipGetLastError();
 }

@@ -114,3 +114,104 @@ def render_frame(render_tiles: Callable[[object], object], height: int, rank: in
         return frame
     dist.gather(part, None, dst=0, group=group)
     return None
+
+
+def assemble_into(frame_padded, gathered, world: int, tile_rows: int = TILE_ROWS):
+    """Re-interleave a (world, slot_rows, W, C) gather result into
+    `frame_padded` ((world * slot_rows, W, C), image order, the last rows
+    padding) with ONE strided copy: tile j*world + r lives in gathered[r, j]."""
+    w, c = gathered.shape[-2], gathered.shape[-1]
+    tpr = gathered.shape[1] // tile_rows
+    src = gathered.reshape(world, tpr, tile_rows, w, c)
+    dst = frame_padded.view(tpr, world, tile_rows, w, c)
+    if hasattr(dst, "copy_"):
+        dst.copy_(src.transpose(0, 1))
+    else:  # numpy
+        dst[...] = src.transpose(1, 0, 2, 3, 4)
+    return frame_padded
+
+
+class FramePipeline:
+    """Row-tile frames over `world` ranks, `depth` frames in flight.
+
+    Step k: this rank renders its tiles of frame k into part buffer k % depth
+    (on the current stream), the gather of that buffer to rank 0 is issued
+    asynchronously (torch.distributed, backend "nccl" = RCCL: it runs on RCCL's
+    own stream after the render), and rank 0 re-interleaves it on a side
+    stream once the gather has landed.  So the gather and the re-interleave
+    of frame k overlap the render of frame k+1; a buffer is reused only after
+    its previous frame's gather (and, on rank 0, re-interleave) finished.
+    `flush()` completes every frame in flight.  On CPU tensors (gloo) the
+    same sequence runs synchronously, and `on_frame(k, frame)` (rank 0) sees
+    each assembled frame.  One collective per frame: the gather."""
+
+    def __init__(self, part_shape, height: int, rank: int, world: int, tile_rows: int = TILE_ROWS,
+                 device=None, depth: int = 2, group=None, on_frame=None):
+        import torch
+
+        self.H, self.rank, self.world, self.T, self.group = height, rank, world, tile_rows, group
+        self.depth, self.on_frame = depth, on_frame
+        self.cuda = device is not None and torch.device(device).type == "cuda"
+        kw = dict(dtype=torch.uint8, device=device)
+        self.parts = [torch.zeros(part_shape, **kw) for _ in range(depth)]
+        self.works = [None] * depth
+        self.frames = [None] * depth          # frame index held by each buffer
+        self.asm_done = [None] * depth        # rank 0, CUDA: re-interleave finished (event)
+        if rank == 0:
+            self.gathered = [torch.empty((world,) + tuple(part_shape), **kw) for _ in range(depth)]
+            self.frame_padded = torch.empty((world * part_shape[0],) + tuple(part_shape[1:]), **kw)
+            self.side = torch.cuda.Stream(device) if self.cuda else None
+        self.k = 0
+
+    @property
+    def frame(self):
+        """Rank 0's latest assembled frame (image order, `height` rows)."""
+        return self.frame_padded[:self.H]
+
+    def _retire(self, b):
+        """Make buffer b reusable: its frame's gather (+ rank 0's re-interleave) done."""
+        import torch
+
+        w = self.works[b]
+        if w is None:
+            return
+        if self.cuda:
+            if self.rank == 0:
+                torch.cuda.current_stream().wait_event(self.asm_done[b])
+            else:
+                w.wait()
+        self.works[b] = None
+
+    def step(self, render):
+        """Enqueue one frame: `render(part)` writes this rank's tiles into `part`."""
+        import torch
+        import torch.distributed as dist
+
+        b = self.k % self.depth
+        self._retire(b)
+        part = self.parts[b]
+        render(part)
+        bufs = list(self.gathered[b].unbind(0)) if self.rank == 0 else None
+        work = dist.gather(part, bufs, dst=0, group=self.group, async_op=True)
+        self.works[b], self.frames[b] = work, self.k
+        if self.rank == 0:
+            if self.cuda:
+                with torch.cuda.stream(self.side):
+                    work.wait()  # side stream waits for the gather
+                    assemble_into(self.frame_padded, self.gathered[b], self.world, self.T)
+                    ev = torch.cuda.Event()
+                    ev.record(self.side)
+                    self.asm_done[b] = ev
+            else:
+                work.wait()
+                assemble_into(self.frame_padded, self.gathered[b], self.world, self.T)
+                if self.on_frame is not None:
+                    self.on_frame(self.k, self.frame)
+        elif not self.cuda:
+            work.wait()
+        self.k += 1
+
+    def flush(self):
+        """Complete every frame in flight (the current stream then holds them all)."""
+        for b in range(self.depth):
+            self._retire(b)

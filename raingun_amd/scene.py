@@ -273,6 +273,11 @@ class DeviceScene:
         """Tile scheduling: True/1 probe-ordered, False/0 raster, -1 auto (include/raingun_debug.h)."""
         _abi.check(_abi.lib().rg_debug_set_tile_order(self.handle, int(mode)))
 
+    def set_lane_depth(self, min_depth: int) -> None:
+        """Rays at recursion depth >= min_depth walk the BVH per lane (0: all
+        non-primary rays, large: none, -1: default) (include/raingun_debug.h)."""
+        _abi.check(_abi.lib().rg_debug_set_lane_depth(self.handle, int(min_depth)))
+
     def bvh_info(self) -> _abi.rg_bvh_info:
         info = _abi.rg_bvh_info()
         _abi.check(_abi.lib().rg_debug_bvh_info(self.handle, C.byref(info)))

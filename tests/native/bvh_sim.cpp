@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 #include "../../raingun_amd/csrc/rg_bvh.h"
@@ -114,8 +115,24 @@ static Hit bvh_trace(const Scene &S, const double o[3], const double d[3], doubl
     return h;
 }
 
-// per-lane walk of the threaded layout (RgBvhLane), as bvh_lane in the kernel
+// per-lane nearest-first walk with a bounded stack, as bvh_lane in the kernel:
+// entries = f32 bits of the entry distance with the low RG_LANE_NODE_BITS
+// cleared | node; a popped entry is skipped when its (lower-bound) distance
+// exceeds the current bound.  Stack overflow is a failure (the host sizes the
+// stack to lane_stack_need, so it must never happen).
 static long g_lane_steps = 0;
+static int g_lane_max_sp = 0;
+static uint32_t lane_key(float tn, int node) {
+    uint32_t b;
+    std::memcpy(&b, &tn, 4);
+    return (b & ~((1u << RG_LANE_NODE_BITS) - 1u)) | (uint32_t)node;
+}
+static float lane_key_t(uint32_t e) {
+    const uint32_t b = e & ~((1u << RG_LANE_NODE_BITS) - 1u);
+    float f;
+    std::memcpy(&f, &b, 4);
+    return f;
+}
 static Hit lane_trace(const Scene &S, const double o[3], const double d[3], double ld, double t0s, bool &any) {
     const double ob[3] = {o[0] + d[0] * t0s, o[1] + d[1] * t0s, o[2] + d[2] * t0s};
     const RayB rb = t0s > 0.0 ? rg_make_rayb(ob[0], ob[1], ob[2], d[0], d[1], d[2])
@@ -123,20 +140,44 @@ static Hit lane_trace(const Scene &S, const double o[3], const double d[3], doub
     Hit h{0.0, -1};
     any = false;
     const bool shadow = ld >= 0.0;
-    int node = 0;
+    const int cap = S.bvh.lane_stack;
+    uint32_t stack[RG_LANE_STACK_MAX];
+    int sp = 0, node = 0;
+    const uint32_t mask = (1u << RG_LANE_NODE_BITS) - 1u;
     while (node >= 0) {
         ++g_lane_steps;
-        const RgBvhLane &N = S.bvh.lane[node];
-        if (N.sph < 0) {
-            const float tb = shadow ? bound(ld - t0s) : (h.id >= 0 ? bound(h.t - t0s) : HUGE_VALF);
-            node = rg_box_hit(N.a, N.b, rb, tb) ? node + 1 : N.miss;
-        } else {
-            double t;
-            if (sphere_exact(&S.sp_bvh[4 * N.sph], o, d, t)) {
-                if (shadow) { if (!(t > ld)) { any = true; return h; } }
-                else add(h, t, (int)S.bvh.order[N.sph]);
+        const RgBvhNode &N = S.bvh.nodes[node];
+        const float tb = shadow ? bound(ld - t0s) : (h.id >= 0 ? bound(h.t - t0s) : HUGE_VALF);
+        uint32_t e[4] = {~0u, ~0u, ~0u, ~0u};
+        for (int k = 0; k < N.nchild; ++k) {
+            float tn;
+            if (!rg_child_hit(N, k, rb, tb, tn)) continue;
+            if (N.child[k] < 0) {
+                const int v = ~N.child[k], first = v >> 3, count = (v & 7) + 1;
+                for (int j = first; j < first + count; ++j) {
+                    double t;
+                    if (sphere_exact(&S.sp_bvh[4 * j], o, d, t)) {
+                        if (shadow) { if (!(t > ld)) { any = true; return h; } }
+                        else add(h, t, (int)S.bvh.order[j]);
+                    }
+                }
+            } else {
+                e[k] = lane_key(tn, N.child[k]);
             }
-            node = N.miss;
+        }
+        std::sort(e, e + 4);
+        for (int i = 3; i >= 1; --i) {
+            if (e[i] == ~0u) continue;
+            if (sp >= cap) { std::fprintf(stderr, "lane stack overflow (cap %d)\n", cap); std::exit(3); }
+            stack[sp++] = e[i];
+            g_lane_max_sp = std::max(g_lane_max_sp, sp);
+        }
+        const float tbn = shadow ? bound(ld - t0s) : (h.id >= 0 ? bound(h.t - t0s) : HUGE_VALF);
+        if (e[0] != ~0u && (shadow || !(lane_key_t(e[0]) > tbn))) { node = (int)(e[0] & mask); continue; }
+        node = -1;
+        while (sp > 0) {
+            const uint32_t x = stack[--sp];
+            if (shadow || !(lane_key_t(x) > tbn)) { node = (int)(x & mask); break; }
         }
     }
     return h;
@@ -186,9 +227,10 @@ int main(int argc, char **argv) {
                 }
             }
     for (int j = 0; j < n; ++j) if (seen[j] != 1) { std::fprintf(stderr, "leaf cover\n"); return 1; }
-    std::vector<int> lseen(n, 0);
-    for (const RgBvhLane &l : S.bvh.lane) if (l.sph >= 0) ++lseen[l.sph];
-    for (int j = 0; j < n; ++j) if (lseen[j] != 1) { std::fprintf(stderr, "lane leaf cover\n"); return 1; }
+    if (S.bvh.nodes.size() > (1u << RG_LANE_NODE_BITS) || S.bvh.lane_stack > RG_LANE_STACK_MAX) {
+        std::fprintf(stderr, "tree too large for the per-lane walk\n");
+        return 1;
+    }
     }
 
     long rays = 0, fallback = 0, mism = 0, hits = 0, shadow_rays = 0, occluded = 0, shifted = 0, nosphere = 0, grown = 0;
@@ -287,10 +329,11 @@ int main(int argc, char **argv) {
     std::printf("{\"spheres\": %d, \"nodes\": %zu, \"leaves\": %d, \"depth\": %d, \"margin\": %.6g, \"obound\": %.6g, "
                 "\"rays\": %ld, \"fallback\": %ld, \"hits\": %ld, \"shadow_rays\": %ld, \"occluded\": %ld, "
                 "\"shifted\": %ld, \"no_sphere\": %ld, \"grown\": %ld, "
-                "\"exact_tests_per_ray\": %.3f, \"nodes_per_ray\": %.3f, \"lane_steps_per_ray\": %.3f, \"mismatches\": %ld}\n",
+                "\"exact_tests_per_ray\": %.3f, \"nodes_per_ray\": %.3f, \"lane_steps_per_ray\": %.3f, "
+                "\"lane_stack\": %d, \"lane_stack_used\": %d, \"mismatches\": %ld}\n",
                 n, S.bvh.nodes.size(), S.bvh.leaves, S.bvh.depth, S.bvh.margin, (double)S.bvh.obound, rays, fallback,
                 hits, shadow_rays, occluded, shifted, nosphere, grown, (double)g_tests / (double)(4 * (rays - fallback)),
                 (double)g_nodes / (double)(4 * (rays - fallback)), (double)g_lane_steps / (double)(4 * (rays - fallback)),
-                mism);
+                S.bvh.lane_stack, g_lane_max_sp, mism);
     return mism ? 1 : 0;
 }

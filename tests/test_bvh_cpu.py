@@ -3,7 +3,8 @@ test rg_bvh_ray.h): tests/native/bvh_sim.cpp traces primary, surface-origin,
 grazing (r(1 +- 1e-9), r(1 +- 1e-13)) and far-origin rays (up to 1e5 x the
 scene, through the clipped-start path of rg_bvh_classify) through the BVH and
 through the brute-force reference scan; closest hits (t bits, YAML index) and
-shadow any-hit answers must agree on every ray.  A negative control shrinks the
+shadow any-hit answers must agree on every ray, for both the wave-coherent walk
+and the per-lane nearest-first walk (bounded stack, pruning at pop).  A negative control shrinks the
 boxes and must be caught."""
 import json
 import os
@@ -55,6 +56,9 @@ def test_bvh_matches_brute_force(sim, args):
     assert res["grown"] > 100  # very far origins: boxes grown by the exact test's slack
     if args[0] >= 1024:  # the point of the structure: a handful of exact tests per ray
         assert res["exact_tests_per_ray"] < 16 and res["nodes_per_ray"] < 16
+        assert res["lane_steps_per_ray"] < 16  # the per-lane nearest-first walk prunes as well
+    # the per-lane walk's stack stays within the bound the host sizes it to
+    assert 0 < res["lane_stack_used"] <= res["lane_stack"] <= 16
 
 
 def test_degenerate_and_clustered_spheres(sim):

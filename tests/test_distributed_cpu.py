@@ -74,3 +74,53 @@ def test_assemble_index_math():
     tparts = [torch.from_numpy(p) for p in parts]
     assert torch.equal(rd.assemble(tparts, H, world, T), torch.from_numpy(img))
     assert tiles == 7 and rd.tiles_per_rank(H, world, T) == 3
+
+
+def _pipe_worker(rank, world, port, W, H, T, K, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from raingun_amd.scene import SceneDesc, load_scene
+        from pathlib import Path
+        g = Path(__file__).resolve().parent / "golden"
+        desc = SceneDesc(load_scene(g / "examples" / "test2.yml", texture_root=g))
+        t = rd.tiling(rank, world, T)
+        st, rgba, _, _, _ = oracle.render(desc, W, H, t.tile_rows, t.tile_stride, t.tile_offset, threads=2)
+        assert st == 0
+        got = {}
+        pipe = rd.FramePipeline((rd.slot_rows(H, world, T), W, 4), H, rank, world, T, device=None,
+                                on_frame=lambda k, f: got.__setitem__(k, f.numpy().copy()))
+        for k in range(K):
+            def render(part, k=k):  # frame k: the rank's tiles with every byte offset by k
+                part.zero_()
+                part[:rgba.shape[0]] = torch.from_numpy((rgba.astype(np.int32) + k).astype(np.uint8))
+            pipe.step(render)
+        pipe.flush()
+        if rank == 0:
+            np.save(out_path, np.stack([got[k] for k in range(K)]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,T", [(2, 16), (3, 8)])
+def test_frame_pipeline_gathers_every_frame(oracle_lib, example_scenes, world, T, tmp_path):
+    """The multi-frame pipeline (double-buffered parts, async gather, re-interleave
+    into the padded frame) delivers each frame k intact and in order."""
+    from raingun_amd.scene import SceneDesc
+    W, H, K = 96, 70, 5
+    _, whole, _, _, _ = oracle_lib.render(SceneDesc(example_scenes["test2"]), W, H)
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_pipe_worker, args=(world, _free_port(), W, H, T, K, out), nprocs=world, join=True)
+    frames = np.load(out)
+    for k in range(K):
+        assert np.array_equal(frames[k], (whole.astype(np.int32) + k).astype(np.uint8)), k
+
+
+def test_assemble_into_matches_assemble():
+    H, world, T, W = 50, 3, 8, 5
+    slot = rd.slot_rows(H, world, T)
+    g = torch.randint(0, 255, (world, slot, W, 4), dtype=torch.uint8)
+    fp = torch.empty((world * slot, W, 4), dtype=torch.uint8)
+    rd.assemble_into(fp, g, world, T)
+    assert torch.equal(fp[:H], rd.assemble(list(g.unbind(0)), H, world, T))

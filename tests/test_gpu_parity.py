@@ -26,9 +26,11 @@ def _device():
     assert lib.rg_device_count() > 0, "no HIP device visible"
 
 
-def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0, path=None, bvh=None):
+def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0, path=None, bvh=None, lane=None):
     desc = SceneDesc(scene)
     ds = DeviceScene(scene, path=path, bvh=bvh)
+    if lane is not None:
+        ds.set_lane_depth(lane)
     st = _abi.rg_stats()
     g_rgba, g_rgb = ds.render_tiles(w, h, tile_rows, stride, offset, want_rgb=True, stats=st)
     o_st, o_rgba, o_rgb, o_counts, o_err = oracle_lib.render(desc, w, h, tile_rows, stride, offset, want_rgb=True)
@@ -43,9 +45,12 @@ def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0, path=None
 
 
 PATHS = [_abi.PATH_LIGHT, _abi.PATH_HEAVY]  # both kernel paths on every scene
-# (kernel path, sphere BVH): the light path never traverses; the heavy path
-# with >= 16 spheres traverses the BVH by default
-PATH_BVH = [(_abi.PATH_LIGHT, False), (_abi.PATH_HEAVY, False), (_abi.PATH_HEAVY, True)]
+# (kernel path, sphere BVH, per-lane walk depth): the light path never
+# traverses; the heavy path with >= 16 spheres traverses the BVH by default,
+# rays of depth >= 1 per lane; lane depth 0 = every non-primary ray per lane,
+# 99 = wave-coherent walk only
+PATH_BVH = [(_abi.PATH_LIGHT, False, None), (_abi.PATH_HEAVY, False, None), (_abi.PATH_HEAVY, True, None),
+            (_abi.PATH_HEAVY, True, 0), (_abi.PATH_HEAVY, True, 99)]
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -88,9 +93,9 @@ def test_config3_test3_4k(oracle_lib, example_scenes):
     (200, 2, 2, 160, 90),
     (40, 4, 20, 160, 90),
 ])
-@pytest.mark.parametrize("path,bvh", PATH_BVH)
-def test_synthetic(oracle_lib, n, planes, depth, w, h, path, bvh):
-    _compare(oracle_lib, synthetic_scene(n, planes, depth), w, h, path=path, bvh=bvh)
+@pytest.mark.parametrize("path,bvh,lane", PATH_BVH)
+def test_synthetic(oracle_lib, n, planes, depth, w, h, path, bvh, lane):
+    _compare(oracle_lib, synthetic_scene(n, planes, depth), w, h, path=path, bvh=bvh, lane=lane)
 
 
 def test_bvh_is_built_for_sphere_scenes():
@@ -106,18 +111,19 @@ def test_bvh_is_built_for_sphere_scenes():
     small.close()
 
 
-@pytest.mark.parametrize("bvh", [True, False])
-def test_config5_shape_4096_spheres_8_planes(oracle_lib, bvh):
+@pytest.mark.parametrize("bvh,lane", [(True, None), (True, 0), (True, 99), (False, None)])
+def test_config5_shape_4096_spheres_8_planes(oracle_lib, bvh, lane):
     """BASELINE configs[4]'s scene (4096 spheres + 8 planes, depth 8; the sphere
     tables exceed LDS, so the BVH kernel reads nodes through the scalar cache)
     at a reduced resolution the CPU restatement finishes quickly."""
-    _compare(oracle_lib, synthetic_scene(4096, 8, 8), 256, 144, path=_abi.PATH_HEAVY, bvh=bvh)
+    _compare(oracle_lib, synthetic_scene(4096, 8, 8), 256, 144, path=_abi.PATH_HEAVY, bvh=bvh, lane=lane)
 
 
-def test_north_star_scene_4k_bvh(oracle_lib):
+@pytest.mark.parametrize("lane", [None, 0])
+def test_north_star_scene_4k_bvh(oracle_lib, lane):
     """The north-star scene (1024 spheres) at the full 3840x2160, depth 5,
     every 9th 16-row tile (the restatement scans all 1026 bodies per ray)."""
-    _compare(oracle_lib, synthetic_scene(1024, 2, 5), 3840, 2160, 16, 9, 4)
+    _compare(oracle_lib, synthetic_scene(1024, 2, 5), 3840, 2160, 16, 9, 4, lane=lane)
 
 
 def test_odd_sizes_and_square(oracle_lib, example_scenes):
@@ -239,13 +245,15 @@ def test_f32_prefilter_tangent_rays(oracle_lib, scale):
         rays.append(np.concatenate([o, d]))
         targets.append(k)
     rays, targets = np.array(rays), np.array(targets)
-    for path, bvh in PATH_BVH:
+    for path, bvh, lane in PATH_BVH:  # rg_trace walks per lane at lane depth <= 1
         ds = DeviceScene(s, path=path, bvh=bvh)
+        if lane is not None:
+            ds.set_lane_depth(lane)
         gd, gb = ds.trace(rays)
         ds.close()
         st, od, ob = oracle_lib.trace(SceneDesc(s), rays)
         assert st == 0
-        assert np.array_equal(gb, ob), f"path {path} bvh {bvh}: {np.count_nonzero(gb != ob)} rays differ"
+        assert np.array_equal(gb, ob), f"path {path} bvh {bvh} lane {lane}: {np.count_nonzero(gb != ob)} rays differ"
         hit = ob >= 0
         assert np.array_equal(gd[hit], od[hit])
     # where nothing else is in the way, grazing rays split between hitting and
