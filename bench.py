@@ -150,32 +150,52 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
     slot = rd.slot_rows(H, world, TILE_ROWS)  # equal-size gather slots (last ranks zero-padded)
     out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
-    gathered = rd.gather_buffers(out, world) if (world > 1 and rank == 0) else None
-    frame = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
+    use_pipe = (world > 1 or args.pipeline) and args.backend == "nccl"
+    gathered = rd.gather_buffers(out, world) if (world > 1 and rank == 0 and not use_pipe) else None
+    frame = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if (rank == 0 and not use_pipe) else None
 
     stream = torch.cuda.current_stream(dev)
     sh = C.c_void_p(stream.cuda_stream)
     events = []          # (start, end) around each timed launch, on the render stream
     max_events = [0]
 
-    def render(stats=None):
-        st = lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(out.data_ptr()), None, sh,
+    def render(stats=None, buf=None):
+        dst = out if buf is None else buf
+        st = lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(dst.data_ptr()), None, sh,
                                        C.byref(stats) if stats is not None else None)
         _abi.check(st, "rg_render_tiles_async")
 
-    def render_tiles(_t):
+    def render_timed(buf=None):
         if len(events) < max_events[0]:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            render()
+            render(buf=buf)
             e1.record(stream)
             events.append((e0, e1))
         else:
-            render()
+            render(buf=buf)
+
+    def render_tiles(_t):
+        render_timed()
         return out
 
+    # N > 1 over RCCL: frames pipelined two deep (the gather and rank 0's
+    # re-interleave of frame k overlap the render of frame k+1; every frame is
+    # complete when the timed region ends).  The gloo rehearsal gathers through
+    # host memory one frame at a time.
+    pipe = None
+    if use_pipe:
+        pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TILE_ROWS, device=dev)
+
     def step():
-        rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
+        if pipe is not None:
+            pipe.step(render_timed)
+        else:
+            rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
+
+    def finish():
+        if pipe is not None:
+            pipe.flush()
 
     # one counted render: ray totals per class (deterministic per frame)
     stats = _abi.rg_stats()
@@ -189,6 +209,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
 
     for _ in range(args.warmup):
         step()
+    finish()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -198,6 +219,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    finish()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -211,7 +233,12 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     elapsed = float(tt[0])
     verified = None
     if getattr(args, "verify", False):
-        final = rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
+        if pipe is not None:
+            step()
+            finish()
+            final = pipe.frame if rank == 0 else None
+        else:
+            final = rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
         if rank == 0:
             torch.cuda.synchronize(dev)
             ref = ds.render_image(W, H)
@@ -237,7 +264,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         "data": src,
         "config": {"workload": label, "width": W, "height": H, "max_recursion_depth": scene.max_recursion_depth,
                    "bodies": body_counts, "lights": len(scene.lights), "tile_rows": TILE_ROWS,
-                   "parallelism": f"row-tiles x{world} (round-robin 16-row tiles, RCCL gather to rank 0)"},
+                   "parallelism": f"row-tiles x{world} (round-robin 16-row tiles, RCCL gather to rank 0"
+                   + (", 2 frames in flight)" if pipe is not None else ")")},
         "rays_per_frame": {"primary": rays[0], "shadow": rays[1], "secondary": rays[2], "total": rays_per_frame},
         "roofline": {
             "bound": "valu_fp64",
@@ -288,9 +316,16 @@ def main() -> None:
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo: rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank renders on GPU 0 (use with --backend gloo)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="rehearsal: run the N>1 frame pipeline (RCCL gather, overlapped re-interleave) at N=1")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 checks the gathered frame against a 1-rank render, byte for byte")
     args = ap.parse_args()
+    # the JSON line is the only thing on stdout: library banners (RCCL prints its
+    # version block on stdout when a communicator is created) go to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
@@ -300,7 +335,11 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.same_device:
         local_rank = 0
-    if world > 1:
+    if world > 1 or args.pipeline:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local_rank)
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -333,8 +372,8 @@ def main() -> None:
         line.update({k: v for k, v in main_res.items() if k not in ("value", "ms_per_step")})
         if ns_res is not None:
             line["north_star_1024_spheres"] = ns_res
-        print(json.dumps(line), flush=True)
-    if world > 1:
+        print(json.dumps(line), file=json_out, flush=True)
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -31,8 +31,10 @@ namespace rgk {
 constexpr double SHADOW_BIAS = 1e-13;                 // lib.rs:11
 constexpr float PI_F = 3.14159265358979323846f;       // std::f32::consts::PI
 
-enum : int { MODE_CLOSEST = 0, MODE_SHADOW = 1, MODE_DONE = 2 };
-enum : int { FR_REFL = 0, FR_REFR_T = 1, FR_REFR_R = 2, FR_REFL_PEND = 3 };
+// MODE_WAIT: the lane's top frame awaits a subtree another lane is tracing (task splitting)
+enum : int { MODE_CLOSEST = 0, MODE_SHADOW = 1, MODE_DONE = 2, MODE_WAIT = 3 };
+// FR_REFR_TASK / FR_REFR_WAIT carry their pool slot in bits 8+ of Frame::type
+enum : int { FR_REFL = 0, FR_REFR_T = 1, FR_REFR_R = 2, FR_REFL_PEND = 3, FR_REFR_TASK = 4, FR_REFR_WAIT = 5 };
 
 struct V3 { double x, y, z; };
 struct C3 { float r, g, b; };
@@ -1063,6 +1065,107 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
     return v;
 }
 
+// ---------------------------------------------------------------- task splitting
+// A refractive hit opens two independent subtrees (transmission, then
+// reflection: rendering.rs:100-113); the lane traces the transmission ray and
+// PUBLISHES the reflection ray in a block-local pool in LDS.  Any idle lane of
+// the block (its pixel finished, or its wave out of tiles) may take it, trace
+// the subtree with the same state machine and hand the colour back; if nobody
+// took it by the time the owner needs it, the owner reclaims it and traces it
+// itself.  A subtree's colour is a function of its ray only, and the owner
+// combines it with exactly the expression of FR_REFR_R, so results are
+// identical whoever traces it.  This splits the long ray trees of
+// refractive pixels (the slowest tiles, which bound a frame's makespan)
+// across the waves of a CU.  Waits only ever point down a tree, so there is
+// no cycle: every awaited subtree is held by a live lane.
+#ifndef RG_LIGHT_TASKS
+#define RG_LIGHT_TASKS 0   // task splitting on the light path (kernel template parameter TASKS)
+#endif
+#ifndef RG_HEAVY_TASKS
+#define RG_HEAVY_TASKS 1   // ... and on the heavy path
+#endif
+#define RG_TASK_SLOTS 128
+struct TaskPool {
+    double ray[RG_TASK_SLOTS][6];  // published ray (origin, direction)
+    float col[RG_TASK_SLOTS][4];   // the subtree's colour once done
+    int depth[RG_TASK_SLOTS];      // recursion depth of the published ray
+    uint32_t pix[RG_TASK_SLOTS];   // owner's pixel (error reports)
+    int done[RG_TASK_SLOTS];       // 1: col holds the result
+    uint32_t free_m[RG_TASK_SLOTS / 32];  // 1 = slot free
+    uint32_t pend_m[RG_TASK_SLOTS / 32];  // 1 = published, not taken
+    int busy;                      // waves of the block that hold work
+};
+__shared__ TaskPool rg_pool;
+
+#define RG_WG __HIP_MEMORY_SCOPE_WORKGROUP
+__device__ __forceinline__ void pool_init() {
+    if (threadIdx.x < RG_TASK_SLOTS / 32) {
+        rg_pool.free_m[threadIdx.x] = ~0u;
+        rg_pool.pend_m[threadIdx.x] = 0u;
+    }
+    if (threadIdx.x < RG_TASK_SLOTS) rg_pool.done[threadIdx.x] = 0;
+    if (threadIdx.x == 0) rg_pool.busy = 0;
+}
+// Claim a free slot (-1: pool full).  Lanes start at different words/bits.
+__device__ __forceinline__ int pool_alloc(int lane) {
+    const int rot = (lane >> 2) & 31;
+    for (int i = 0; i < RG_TASK_SLOTS / 32; ++i) {
+        const int w = (lane + i) & (RG_TASK_SLOTS / 32 - 1);
+        uint32_t m = __hip_atomic_load(&rg_pool.free_m[w], __ATOMIC_RELAXED, RG_WG);
+        while (m != 0u) {
+            const uint32_t r = rot ? ((m >> rot) | (m << (32 - rot))) : m;
+            const int b = (__builtin_ctz(r) + rot) & 31;
+            const uint32_t bit = 1u << b;
+            const uint32_t old = __hip_atomic_fetch_and(&rg_pool.free_m[w], ~bit, __ATOMIC_ACQUIRE, RG_WG);
+            if (old & bit) return w * 32 + b;
+            m = old & ~bit;
+        }
+    }
+    return -1;
+}
+__device__ __forceinline__ void pool_publish(int slot) {  // ray/depth/pix written before
+    __hip_atomic_fetch_or(&rg_pool.pend_m[slot >> 5], 1u << (slot & 31), __ATOMIC_RELEASE, RG_WG);
+}
+__device__ __forceinline__ bool pool_any_pending() {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int w = 0; w < RG_TASK_SLOTS / 32; ++w) m |= __hip_atomic_load(&rg_pool.pend_m[w], __ATOMIC_RELAXED, RG_WG);
+    return m != 0u;
+}
+// Take the k-th pending task of a snapshot (k = rank among the wave's idle lanes).
+__device__ __forceinline__ int pool_take(int k) {
+    for (int w = 0; w < RG_TASK_SLOTS / 32; ++w) {
+        uint32_t m = __hip_atomic_load(&rg_pool.pend_m[w], __ATOMIC_RELAXED, RG_WG);
+        const int n = __builtin_popcount(m);
+        if (k >= n) {
+            k -= n;
+            continue;
+        }
+        for (int j = 0; j < k; ++j) m &= m - 1u;
+        const uint32_t bit = m & (~m + 1u);
+        const uint32_t old = __hip_atomic_fetch_and(&rg_pool.pend_m[w], ~bit, __ATOMIC_ACQUIRE, RG_WG);
+        return (old & bit) ? w * 32 + __builtin_ctz(bit) : -1;
+    }
+    return -1;
+}
+__device__ __forceinline__ bool pool_reclaim(int slot) {  // owner: un-publish if still pending
+    const uint32_t bit = 1u << (slot & 31);
+    return (__hip_atomic_fetch_and(&rg_pool.pend_m[slot >> 5], ~bit, __ATOMIC_ACQ_REL, RG_WG) & bit) != 0u;
+}
+__device__ __forceinline__ void pool_finish(int slot, C3 c) {  // taker: result, then done
+    rg_pool.col[slot][0] = c.r;
+    rg_pool.col[slot][1] = c.g;
+    rg_pool.col[slot][2] = c.b;
+    __hip_atomic_store(&rg_pool.done[slot], 1, __ATOMIC_RELEASE, RG_WG);
+}
+__device__ __forceinline__ bool pool_done(int slot) {
+    return __hip_atomic_load(&rg_pool.done[slot], __ATOMIC_ACQUIRE, RG_WG) != 0;
+}
+__device__ __forceinline__ void pool_release(int slot) {  // owner: slot free again
+    __hip_atomic_store(&rg_pool.done[slot], 0, __ATOMIC_RELAXED, RG_WG);
+    __hip_atomic_fetch_or(&rg_pool.free_m[slot >> 5], 1u << (slot & 31), __ATOMIC_RELEASE, RG_WG);
+}
+
 }  // namespace rgk
 
 using namespace rgk;
@@ -1100,7 +1203,7 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // repeatedly takes the next 8x8 pixel tile from an atomic queue
 // (counters[16..], sharded) and runs the per-lane state machine until its 64 lanes have
 // written their pixels.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH>
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
 __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     static_assert(!BVH || 4 * WPS <= RG_BVH_MAX_WAVES, "one BVH stack per wave");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1150,7 +1253,10 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         T.lights = a.lights;
         T.texs = a.texs;
     }
-    if constexpr (LSPH || LCOLD) __syncthreads();
+    if (TASKS || LSPH || LCOLD) {
+        if constexpr (TASKS) pool_init();
+        __syncthreads();
+    }
 
     const int lane = threadIdx.x & 63;
 #ifdef RG_BVH_STATS
@@ -1176,368 +1282,484 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
 #else
     uint32_t qi = gwave % RG_NQ, qtried = 0;
 #endif
-    for (;;) {
-        uint32_t tile = 0xFFFFFFFFu;
-        while (qtried < RG_NQ) {
-            uint32_t k = 0;
-            if (lane == 0) k = atomicAdd(reinterpret_cast<unsigned int *>(&a.counters[RG_QUEUE_BASE + RG_QUEUE_STRIDE * qi]), 1u);
-            k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
-#if RG_Q_INTERLEAVE
-            // head q serves tiles q, q+NQ, q+2NQ, ...: the tiles in flight stay a
-            // compact raster-order band of the frame, as with a single head
-            const unsigned long long t = (unsigned long long)k * RG_NQ + qi;
-            if (t < ntiles) { tile = (uint32_t)t; break; }
-#else
-            const uint32_t lo = (uint32_t)(((unsigned long long)ntiles * qi) / RG_NQ);
-            const uint32_t hi = (uint32_t)(((unsigned long long)ntiles * (qi + 1)) / RG_NQ);
-            if (lo + k < hi) { tile = lo + k; break; }
-#endif
-            qi = (qi + 1) % RG_NQ;
-            ++qtried;
-        }
-        if (tile == 0xFFFFFFFFu) break;
-        if (a.tile_perm) tile = a.tile_perm[tile];  // scheduling order only; every tile is rendered once
-        const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    // Lane state.  A lane holds one pixel of the wave's 8x8 tile, or (task
+    // splitting, TASKS) one published subtree of another lane of the block;
+    // the wave takes the next tile when none of its lanes has work.
+    int mode = MODE_DONE;
+    Ray q;                 // current query (shadow: q.o = shared origin)
+    ShadowBatch<LB> sb;        // shadow: the batch's directions and light distances
+    uint32_t occl_full = 0u;
+    float pp[LB], lin[LB], refl_f = 0.0f;  // light path: per-light max(n.l, 0), intensity; albedo/pi
+    int qdepth = 0;        // closest: depth of the ray
+    // hit being shaded
+    V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0), hd = v3(0, 0, 0);
+    int hb = 0, hdepth = 0, li = 0;
+    C3 fin = c3(0, 0, 0), bcol = c3(0, 0, 0), ret = def;
+    int sp = 0;
+    Closest c;
+    closest_init(c);
+    bool have_result = false;  // c / occl hold a fresh result for the lane's query
+    uint32_t occl = 0u;
+    size_t oidx = 0;           // output index of the lane's pixel
+    uint32_t pixel = 0;        // image pixel index (error reports) of the lane's pixel or task
+    int task = -1;             // pool slot whose subtree this lane computes (-1: its own pixel)
+    bool tiles_left = true;    // the tile queue has not been found empty
+    [[maybe_unused]] bool counted = false;  // this wave is counted in rg_pool.busy
 #ifdef RG_TILE_TIMES
-        const unsigned long long t_tile = wall_clock64();  // diagnostic: per-tile time into rgb[tile] (us),
-        uint32_t tile_iters = 0;                           // wave iterations into rgb[ntiles + tile]
-        unsigned long long t_query = 0;                    // time in the body/BVH queries into rgb[3 ntiles + tile]
-#ifdef RG_BVH_STATS  // with the BVH statistics: per-tile full-scan / traversal clocks and scan lanes
-        const unsigned long long st0_scan = rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][13];
-        const unsigned long long st0_trav = rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][12];
-        const unsigned long long st0_lanes = rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][8];
-        const unsigned long long st0_trv = rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][4];
-        const unsigned long long st0_steps = rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][5];
+    uint32_t cur_tile = 0xFFFFFFFFu;  // diagnostic: per-tile time into rgb[tile] (us), wave iterations
+    unsigned long long t_tile = 0, t_query = 0;  // into rgb[ntiles + tile], start, query time
+    uint32_t tile_iters = 0;
 #endif
-#endif
-        const uint32_t x = tx * 8u + (uint32_t)(lane & 7);
-        const uint32_t orow = ty * 8u + (uint32_t)(lane >> 3);
-        bool alive = x < a.width && orow < a.out_rows;
-        uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
-        const size_t oidx = (size_t)orow * a.width + x;
-        if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
-            a.rgba[oidx] = 0u;
-#ifndef RG_TILE_TIMES
-            if (a.rgb) { a.rgb[3 * oidx] = 0.0f; a.rgb[3 * oidx + 1] = 0.0f; a.rgb[3 * oidx + 2] = 0.0f; }
-#endif
-            alive = false;
-        }
-        const uint32_t pixel = y * a.width + x;
-
-        int mode = MODE_DONE;
-        Ray q;                 // current query (shadow: q.o = shared origin)
-        ShadowBatch<LB> sb;        // shadow: the batch's directions and light distances
-        uint32_t occl_full = 0u;
-        float pp[LB], lin[LB], refl_f = 0.0f;  // light path: per-light max(n.l, 0), intensity; albedo/pi
-        int qdepth = 0;        // closest: depth of the ray
-        // hit being shaded
-        V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0), hd = v3(0, 0, 0);
-        int hb = 0, hdepth = 0, li = 0;
-        C3 fin = c3(0, 0, 0), bcol = c3(0, 0, 0), ret = def;
-        int sp = 0;
-        Closest c;
-        closest_init(c);
-
-        if (alive) {
-            // ray.rs:37-54 (aspect and fov_adjustment are per-frame constants)
-            double sx = ((((double)x + 0.5) / (double)a.width) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
-            double sy = (1.0 - (((double)y + 0.5) / (double)a.height) * 2.0) * a.fov_adjustment;
-            q.o = v3(0.0, 0.0, 0.0);
-            q.d = normalize(v3(sx, sy, -1.0));
-            n_prim++;
-            trace_primary<F32F, BVH>(a, src, q.d, c);
-            mode = MODE_CLOSEST;
-            qdepth = 0;
-        }
-
-        bool have_result = alive;  // c / occl hold a fresh result for the lane's query
-        uint32_t occl = 0u;
-        for (;;) {
-            if (have_result) {
-                bool unwind = false;
-                bool shade = false;           // run a shade_diffuse step this iteration
-                const int rmode = mode;       // kind of result the lane holds
-                if (rmode == MODE_CLOSEST) {
-                    if (c.nan && c.nhit >= 2) raise_error(a, pixel, RG_ERR_NAN_DISTANCE);
-                    if (c.id < 0) {
-                        ret = def;  // rendering.rs:76-77, 128-129
-                        unwind = true;
-                    } else {
-                        // get_color (rendering.rs:80-120)
-                        const RgBodyDev b = T.bodies[c.id];
-                        const RgMatDev m = T.mats[c.id];
-                        V3 h = add(q.o, scl(q.d, c.t));
-                        V3 n;
-                        if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
-                        if (m.surface != RG_SURFACE_REFRACTIVE) {
-                            bcol = surface_color(T.texs, m, b, h);
-                            hb = c.id; hdepth = qdepth;
-                            if constexpr (LB > 1) {
-                                // ONE batch covers every light (n_lights <= LB on this path): set it
-                                // up now, with the per-light shading factors, so that no hit-point
-                                // state (h, n, incident) has to survive the shadow pass
-                                refl_f = m.albedo / PI_F;                               // rendering.rs:164
-                                if (m.surface == RG_SURFACE_REFLECTING && qdepth + 1 < max_depth) {
-                                    Frame &f = stk[sp++];                               // reflection ray of
-                                    const Ray rr = reflection(n, q.d, h);               // rendering.rs:88,
-                                    f.type = FR_REFL_PEND;                              // D filled in later
-                                    f.rr[0] = rr.o.x; f.rr[1] = rr.o.y; f.rr[2] = rr.o.z;
-                                    f.rr[3] = rr.d.x; f.rr[4] = rr.d.y; f.rr[5] = rr.d.z;
-                                    f.f[3] = m.reflectivity;
-                                    f.cdepth = qdepth + 1;
-                                }
-                                q.o = add(h, scl(n, SHADOW_BIAS));                      // rendering.rs:148
-                                occl_full = 0u;
+    for (;;) {
+        if (have_result) {
+            bool unwind = false;
+            bool shade = false;           // run a shade_diffuse step this iteration
+            const int rmode = mode;       // kind of result the lane holds
+            if (rmode == MODE_WAIT) {
+                unwind = true;  // poll the awaited subtree (top frame FR_REFR_WAIT)
+            } else if (rmode == MODE_CLOSEST) {
+                if (c.nan && c.nhit >= 2) raise_error(a, pixel, RG_ERR_NAN_DISTANCE);
+                if (c.id < 0) {
+                    ret = def;  // rendering.rs:76-77, 128-129
+                    unwind = true;
+                } else {
+                    // get_color (rendering.rs:80-120)
+                    const RgBodyDev b = T.bodies[c.id];
+                    const RgMatDev m = T.mats[c.id];
+                    V3 h = add(q.o, scl(q.d, c.t));
+                    V3 n;
+                    if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
+                    if (m.surface != RG_SURFACE_REFRACTIVE) {
+                        bcol = surface_color(T.texs, m, b, h);
+                        hb = c.id; hdepth = qdepth;
+                        if constexpr (LB > 1) {
+                            // ONE batch covers every light (n_lights <= LB on this path): set it
+                            // up now, with the per-light shading factors, so that no hit-point
+                            // state (h, n, incident) has to survive the shadow pass
+                            refl_f = m.albedo / PI_F;                               // rendering.rs:164
+                            if (m.surface == RG_SURFACE_REFLECTING && qdepth + 1 < max_depth) {
+                                Frame &f = stk[sp++];                               // reflection ray of
+                                const Ray rr = reflection(n, q.d, h);               // rendering.rs:88,
+                                f.type = FR_REFL_PEND;                              // D filled in later
+                                f.rr[0] = rr.o.x; f.rr[1] = rr.o.y; f.rr[2] = rr.o.z;
+                                f.rr[3] = rr.d.x; f.rr[4] = rr.d.y; f.rr[5] = rr.d.z;
+                                f.f[3] = m.reflectivity;
+                                f.cdepth = qdepth + 1;
+                            }
+                            q.o = add(h, scl(n, SHADOW_BIAS));                      // rendering.rs:148
+                            occl_full = 0u;
 #pragma unroll
-                                for (int l = 0; l < LB; ++l) {
-                                    if (l < a.n_lights) {
-                                        const RgLightDev L = T.lights[l];
-                                        light_dir_dist(L, h, sb.d[l], sb.ld[l]);
-                                        pp[l] = fmaxf((float)dot(n, sb.d[l]), 0.0f);    // rendering.rs:161-162
-                                        lin[l] = light_intensity(L, h);                 // pure; used if lit
-                                        occl_full |= 1u << l;
-                                        n_shadow++;
-                                    } else {
-                                        sb.d[l] = v3(0.0, 0.0, 1.0);
-                                        sb.ld[l] = 0.0;
-                                        pp[l] = 0.0f;
-                                        lin[l] = 0.0f;
+                            for (int l = 0; l < LB; ++l) {
+                                if (l < a.n_lights) {
+                                    const RgLightDev L = T.lights[l];
+                                    light_dir_dist(L, h, sb.d[l], sb.ld[l]);
+                                    pp[l] = fmaxf((float)dot(n, sb.d[l]), 0.0f);    // rendering.rs:161-162
+                                    lin[l] = light_intensity(L, h);                 // pure; used if lit
+                                    occl_full |= 1u << l;
+                                    n_shadow++;
+                                } else {
+                                    sb.d[l] = v3(0.0, 0.0, 1.0);
+                                    sb.ld[l] = 0.0;
+                                    pp[l] = 0.0f;
+                                    lin[l] = 0.0f;
+                                }
+                            }
+                            if (a.n_lights > 0) mode = MODE_SHADOW;
+                            else shade = true;  // no lights: finish with black (rendering.rs:138)
+                        } else {
+                            fin = c3(0.0f, 0.0f, 0.0f);
+                            hp = h; hn = n; hd = q.d; li = 0;
+                            shade = true;
+                        }
+                    } else {
+                        float kr = (float)fresnel(q.d, n, m.index);
+                        C3 surf = surface_color(T.texs, m, b, h);
+                        Ray rr = reflection(n, q.d, h);
+                        int cd = qdepth + 1;
+                        C3 tc = def;
+                        bool trace_t = false;
+                        Ray tr;
+                        if (kr < 1.0f) {
+                            if (!transmission(n, q.d, h, m.index, tr)) raise_error(a, pixel, RG_ERR_TRANSMISSION);
+                            else if (cd < max_depth) trace_t = true;
+                        }
+                        if (cd >= max_depth) {
+                            C3 col = cadd(cscl(def, kr), cscl(tc, 1.0f - kr));
+                            ret = cmul(cscl(col, m.transparency), surf);
+                            unwind = true;
+                        } else {
+                            Frame &f = stk[sp++];
+                            f.f[0] = kr; f.f[1] = m.transparency;
+                            f.f[2] = surf.r; f.f[3] = surf.g; f.f[4] = surf.b;
+                            f.f[5] = tc.r; f.f[6] = tc.g; f.f[7] = tc.b;
+                            f.cdepth = cd;
+                            if (trace_t) {
+                                // the reflection subtree waits until the transmission subtree is
+                                // done: publish it, so an idle lane of the block can trace it now
+                                int slot = -1;
+                                if constexpr (TASKS) {
+                                    slot = pool_alloc(lane);
+                                    if (slot >= 0) {
+                                        double *pr = rg_pool.ray[slot];
+                                        pr[0] = rr.o.x; pr[1] = rr.o.y; pr[2] = rr.o.z;
+                                        pr[3] = rr.d.x; pr[4] = rr.d.y; pr[5] = rr.d.z;
+                                        rg_pool.depth[slot] = cd;
+                                        rg_pool.pix[slot] = pixel;
+                                        pool_publish(slot);
+                                        f.type = FR_REFR_TASK | (slot << 8);
                                     }
                                 }
-                                if (a.n_lights > 0) mode = MODE_SHADOW;
-                                else shade = true;  // no lights: finish with black (rendering.rs:138)
-                            } else {
-                                fin = c3(0.0f, 0.0f, 0.0f);
-                                hp = h; hn = n; hd = q.d; li = 0;
-                                shade = true;
-                            }
-                        } else {
-                            float kr = (float)fresnel(q.d, n, m.index);
-                            C3 surf = surface_color(T.texs, m, b, h);
-                            Ray rr = reflection(n, q.d, h);
-                            int cd = qdepth + 1;
-                            C3 tc = def;
-                            bool trace_t = false;
-                            Ray tr;
-                            if (kr < 1.0f) {
-                                if (!transmission(n, q.d, h, m.index, tr)) raise_error(a, pixel, RG_ERR_TRANSMISSION);
-                                else if (cd < max_depth) trace_t = true;
-                            }
-                            if (cd >= max_depth) {
-                                C3 col = cadd(cscl(def, kr), cscl(tc, 1.0f - kr));
-                                ret = cmul(cscl(col, m.transparency), surf);
-                                unwind = true;
-                            } else {
-                                Frame &f = stk[sp++];
-                                f.f[0] = kr; f.f[1] = m.transparency;
-                                f.f[2] = surf.r; f.f[3] = surf.g; f.f[4] = surf.b;
-                                f.f[5] = tc.r; f.f[6] = tc.g; f.f[7] = tc.b;
-                                f.cdepth = cd;
-                                if (trace_t) {
+                                if (slot < 0) {
                                     f.type = FR_REFR_T;
                                     f.rr[0] = rr.o.x; f.rr[1] = rr.o.y; f.rr[2] = rr.o.z;
                                     f.rr[3] = rr.d.x; f.rr[4] = rr.d.y; f.rr[5] = rr.d.z;
-                                    q = tr;
-                                } else {
-                                    f.type = FR_REFR_R;
-                                    q = rr;
                                 }
-                                qdepth = cd;
-                                mode = MODE_CLOSEST;
-                                n_sec++;
+                                q = tr;
+                            } else {
+                                f.type = FR_REFR_R;
+                                q = rr;
                             }
-                        }
-                    }
-                } else {
-                    shade = true;  // a shadow result for light li
-                }
-                if constexpr (LB > 1) {
-                  if (shade) {
-                    // shade_diffuse accumulation over the batch (rendering.rs:141-170), in light order
-                    const RgMatDev m = T.mats[hb];
-                    C3 acc = c3(0.0f, 0.0f, 0.0f);
-#pragma unroll
-                    for (int l = 0; l < LB; ++l) {
-                        if (l < a.n_lights) {
-                            const RgLightDev L = T.lights[l];
-                            const float inten = !((occl >> l) & 1u) ? lin[l] : 0.0f;
-                            const float power = pp[l] * inten;
-                            C3 lc = cscl(cscl(c3(L.color[0], L.color[1], L.color[2]), power), refl_f);
-                            acc = cadd(acc, cmul(bcol, lc));
-                        }
-                    }
-                    C3 dcol = cclamp(acc);
-                    if (m.surface == RG_SURFACE_DIFFUSE) {
-                        ret = dcol;
-                        unwind = true;
-                    } else {  // Reflecting (rendering.rs:86-91)
-                        const float r = m.reflectivity;
-                        const int cd = hdepth + 1;
-                        if (cd >= max_depth) {
-                            ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
-                            unwind = true;
-                        } else {
-                            Frame &f = stk[sp - 1];  // the FR_REFL_PEND pushed at the hit
-                            f.type = FR_REFL;
-                            f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b;
-                            q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
-                            q.d = v3(f.rr[3], f.rr[4], f.rr[5]);
                             qdepth = cd;
                             mode = MODE_CLOSEST;
                             n_sec++;
                         }
                     }
-                  }
-                } else if (shade) {
-                    // shade_diffuse loop body (rendering.rs:141-170), one light per iteration
-                    const RgMatDev m = T.mats[hb];
-                    if (rmode == MODE_SHADOW) {
-                        const float refl = m.albedo / PI_F;
+                }
+            } else if (rmode == MODE_SHADOW) {
+                shade = true;  // a shadow result for light li
+            }
+            if constexpr (LB > 1) {
+              if (shade) {
+                // shade_diffuse accumulation over the batch (rendering.rs:141-170), in light order
+                const RgMatDev m = T.mats[hb];
+                C3 acc = c3(0.0f, 0.0f, 0.0f);
 #pragma unroll
-                        for (int l = 0; l < LB; ++l) {
-                            if (li + l < a.n_lights) {
-                                const RgLightDev L = T.lights[li + l];
-                                float inten = !((occl >> l) & 1u) ? light_intensity(L, hp) : 0.0f;
-                                float power = fmaxf((float)dot(hn, sb.d[l]), 0.0f) * inten;
-                                C3 lc = cscl(cscl(c3(L.color[0], L.color[1], L.color[2]), power), refl);
-                                fin = cadd(fin, cmul(bcol, lc));
-                            }
-                        }
-                        li += LB;
+                for (int l = 0; l < LB; ++l) {
+                    if (l < a.n_lights) {
+                        const RgLightDev L = T.lights[l];
+                        const float inten = !((occl >> l) & 1u) ? lin[l] : 0.0f;
+                        const float power = pp[l] * inten;
+                        C3 lc = cscl(cscl(c3(L.color[0], L.color[1], L.color[2]), power), refl_f);
+                        acc = cadd(acc, cmul(bcol, lc));
                     }
-                    if (li < a.n_lights) {
-                        q.o = add(hp, scl(hn, SHADOW_BIAS));  // rendering.rs:148
-                        occl_full = 0u;
-#pragma unroll
-                        for (int l = 0; l < LB; ++l) {
-                            if (li + l < a.n_lights) {
-                                light_dir_dist(T.lights[li + l], hp, sb.d[l], sb.ld[l]);
-                                occl_full |= 1u << l;
-                                n_shadow++;
-                            } else {
-                                sb.d[l] = v3(0.0, 0.0, 1.0);
-                                sb.ld[l] = 0.0;
-                            }
-                        }
-                        mode = MODE_SHADOW;
+                }
+                C3 dcol = cclamp(acc);
+                if (m.surface == RG_SURFACE_DIFFUSE) {
+                    ret = dcol;
+                    unwind = true;
+                } else {  // Reflecting (rendering.rs:86-91)
+                    const float r = m.reflectivity;
+                    const int cd = hdepth + 1;
+                    if (cd >= max_depth) {
+                        ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
+                        unwind = true;
                     } else {
-                        C3 dcol = cclamp(fin);
-                        if (m.surface == RG_SURFACE_DIFFUSE) {
-                            ret = dcol;
+                        Frame &f = stk[sp - 1];  // the FR_REFL_PEND pushed at the hit
+                        f.type = FR_REFL;
+                        f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b;
+                        q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
+                        q.d = v3(f.rr[3], f.rr[4], f.rr[5]);
+                        qdepth = cd;
+                        mode = MODE_CLOSEST;
+                        n_sec++;
+                    }
+                }
+              }
+            } else if (shade) {
+                // shade_diffuse loop body (rendering.rs:141-170), one light per iteration
+                const RgMatDev m = T.mats[hb];
+                if (rmode == MODE_SHADOW) {
+                    const float refl = m.albedo / PI_F;
+#pragma unroll
+                    for (int l = 0; l < LB; ++l) {
+                        if (li + l < a.n_lights) {
+                            const RgLightDev L = T.lights[li + l];
+                            float inten = !((occl >> l) & 1u) ? light_intensity(L, hp) : 0.0f;
+                            float power = fmaxf((float)dot(hn, sb.d[l]), 0.0f) * inten;
+                            C3 lc = cscl(cscl(c3(L.color[0], L.color[1], L.color[2]), power), refl);
+                            fin = cadd(fin, cmul(bcol, lc));
+                        }
+                    }
+                    li += LB;
+                }
+                if (li < a.n_lights) {
+                    q.o = add(hp, scl(hn, SHADOW_BIAS));  // rendering.rs:148
+                    occl_full = 0u;
+#pragma unroll
+                    for (int l = 0; l < LB; ++l) {
+                        if (li + l < a.n_lights) {
+                            light_dir_dist(T.lights[li + l], hp, sb.d[l], sb.ld[l]);
+                            occl_full |= 1u << l;
+                            n_shadow++;
+                        } else {
+                            sb.d[l] = v3(0.0, 0.0, 1.0);
+                            sb.ld[l] = 0.0;
+                        }
+                    }
+                    mode = MODE_SHADOW;
+                } else {
+                    C3 dcol = cclamp(fin);
+                    if (m.surface == RG_SURFACE_DIFFUSE) {
+                        ret = dcol;
+                        unwind = true;
+                    } else {  // Reflecting (rendering.rs:86-91)
+                        float r = m.reflectivity;
+                        int cd = hdepth + 1;
+                        if (cd >= max_depth) {
+                            ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
                             unwind = true;
-                        } else {  // Reflecting (rendering.rs:86-91)
-                            float r = m.reflectivity;
-                            int cd = hdepth + 1;
-                            if (cd >= max_depth) {
-                                ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
-                                unwind = true;
-                            } else {
-                                Frame &f = stk[sp++];
-                                f.type = FR_REFL;
-                                f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = r;
-                                f.cdepth = cd;
-                                q = reflection(hn, hd, hp);
-                                qdepth = cd;
-                                mode = MODE_CLOSEST;
-                                n_sec++;
-                            }
+                        } else {
+                            Frame &f = stk[sp++];
+                            f.type = FR_REFL;
+                            f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = r;
+                            f.cdepth = cd;
+                            q = reflection(hn, hd, hp);
+                            qdepth = cd;
+                            mode = MODE_CLOSEST;
+                            n_sec++;
                         }
                     }
                 }
-                if (unwind) {
-                    for (;;) {
-                        if (sp == 0) {
+            }
+            if (unwind) {
+                for (;;) {
+                    if (sp == 0) {
+                        bool handed = false;
+                        if constexpr (TASKS) {
+                            if (task >= 0) {  // a published subtree: hand its colour back
+                                pool_finish(task, ret);
+                                task = -1;
+                                handed = true;
+                            }
+                        }
+                        if (!handed) {
                             a.rgba[oidx] = f32_to_u8(ret.r * 255.0f) | (f32_to_u8(ret.g * 255.0f) << 8) |
                                            (f32_to_u8(ret.b * 255.0f) << 16) | 0xFF000000u;
 #ifndef RG_TILE_TIMES
                             if (a.rgb) { a.rgb[3 * oidx] = ret.r; a.rgb[3 * oidx + 1] = ret.g; a.rgb[3 * oidx + 2] = ret.b; }
 #endif
-                            mode = MODE_DONE;
-                            break;
                         }
-                        Frame &f = stk[sp - 1];
-                        if (f.type == FR_REFL) {
-                            ret = cadd(cscl(c3(f.f[0], f.f[1], f.f[2]), 1.0f - f.f[3]), cscl(ret, f.f[3]));
-                            sp--;
-                        } else if (f.type == FR_REFR_T) {
-                            f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
-                            f.type = FR_REFR_R;
-                            q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
-                            q.d = v3(f.rr[3], f.rr[4], f.rr[5]);
-                            qdepth = f.cdepth;
-                            mode = MODE_CLOSEST;
-                            n_sec++;
-                            break;
-                        } else {  // FR_REFR_R (rendering.rs:115-117)
-                            float kr = f.f[0];
-                            C3 col = cadd(cscl(ret, kr), cscl(c3(f.f[5], f.f[6], f.f[7]), 1.0f - kr));
+                        mode = MODE_DONE;
+                        break;
+                    }
+                    Frame &f = stk[sp - 1];
+                    if constexpr (TASKS) {
+                        const int ftype = f.type & 0xFF;
+                        if (ftype == FR_REFR_TASK || ftype == FR_REFR_WAIT) {
+                            const int slot = f.type >> 8;
+                            if (ftype == FR_REFR_TASK) {  // ret = the transmission subtree's colour
+                                f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
+                                if (pool_reclaim(slot)) {  // nobody took the reflection ray: trace it here
+                                    const double *r = rg_pool.ray[slot];
+                                    q.o = v3(r[0], r[1], r[2]);
+                                    q.d = v3(r[3], r[4], r[5]);
+                                    pool_release(slot);
+                                    f.type = FR_REFR_R;
+                                    qdepth = f.cdepth;
+                                    mode = MODE_CLOSEST;
+                                    n_sec++;
+                                    break;
+                                }
+                                f.type = FR_REFR_WAIT | (slot << 8);
+                            }
+                            if (!pool_done(slot)) {  // another lane is still tracing it
+                                mode = MODE_WAIT;
+                                break;
+                            }
+                            const C3 rc = c3(rg_pool.col[slot][0], rg_pool.col[slot][1], rg_pool.col[slot][2]);
+                            pool_release(slot);
+                            const float kr = f.f[0];  // as FR_REFR_R below (rendering.rs:115-117)
+                            C3 col = cadd(cscl(rc, kr), cscl(c3(f.f[5], f.f[6], f.f[7]), 1.0f - kr));
                             ret = cmul(cscl(col, f.f[1]), c3(f.f[2], f.f[3], f.f[4]));
                             sp--;
+                            continue;
                         }
+                    }
+                    if (f.type == FR_REFL) {
+                        ret = cadd(cscl(c3(f.f[0], f.f[1], f.f[2]), 1.0f - f.f[3]), cscl(ret, f.f[3]));
+                        sp--;
+                    } else if (f.type == FR_REFR_T) {
+                        f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
+                        f.type = FR_REFR_R;
+                        q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
+                        q.d = v3(f.rr[3], f.rr[4], f.rr[5]);
+                        qdepth = f.cdepth;
+                        mode = MODE_CLOSEST;
+                        n_sec++;
+                        break;
+                    } else {  // FR_REFR_R (rendering.rs:115-117)
+                        float kr = f.f[0];
+                        C3 col = cadd(cscl(ret, kr), cscl(c3(f.f[5], f.f[6], f.f[7]), 1.0f - kr));
+                        ret = cmul(cscl(col, f.f[1]), c3(f.f[2], f.f[3], f.f[4]));
+                        sp--;
                     }
                 }
             }
-            const bool live = mode != MODE_DONE;
-            if (!__any(live)) break;
+        }
+        have_result = false;
+        // a wave with no live lane takes the next tile
+        if (tiles_left && !__any(mode != MODE_DONE)) {
 #ifdef RG_TILE_TIMES
-            ++tile_iters;
-#endif
-            if (live) {
-                closest_init(c);
-                occl = 0u;
+            if (cur_tile != 0xFFFFFFFFu && lane == 0 && a.rgb) {
+                a.rgb[cur_tile] = (float)(wall_clock64() - t_tile) * 0.01f;  // 100 MHz clock
+                a.rgb[ntiles + cur_tile] = (float)tile_iters;
+                a.rgb[2 * ntiles + cur_tile] = (float)(t_tile & 0xFFFFFFull);  // start, 24-bit ticks (exact in f32)
+                a.rgb[3 * ntiles + cur_tile] = (float)t_query * 0.01f;
             }
-#ifdef RG_TILE_TIMES
-            const unsigned long long t_q0 = wall_clock64();
+            cur_tile = 0xFFFFFFFFu;
 #endif
-            if constexpr (LB == 1) {
-                // one ray per lane, one pass: closest-hit and shadow lanes share the
-                // body loop (best when a wave mixes ray kinds over many bodies)
-                if (live) {
-                    bool o1 = false;
-                    Ray r1;
-                    r1.o = q.o;
-                    r1.d = mode == MODE_SHADOW ? sb.d[0] : q.d;
-                    const bool lane_walk = (mode == MODE_SHADOW ? hdepth : qdepth) >= (int)a.lane_min_depth;
-                    trace_query<F32F, BVH>(a, src, r1, mode == MODE_SHADOW, sb.ld[0], c, o1, lane_walk);
-                    occl = o1 ? 1u : 0u;
-                }
+            uint32_t tile = 0xFFFFFFFFu;
+            while (qtried < RG_NQ) {
+                uint32_t k = 0;
+                if (lane == 0) k = atomicAdd(reinterpret_cast<unsigned int *>(&a.counters[RG_QUEUE_BASE + RG_QUEUE_STRIDE * qi]), 1u);
+                k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
+#if RG_Q_INTERLEAVE
+                // head q serves tiles q, q+NQ, q+2NQ, ...: the tiles in flight stay a
+                // compact raster-order band of the frame, as with a single head
+                const unsigned long long t = (unsigned long long)k * RG_NQ + qi;
+                if (t < ntiles) { tile = (uint32_t)t; break; }
+#else
+                const uint32_t lo = (uint32_t)(((unsigned long long)ntiles * qi) / RG_NQ);
+                const uint32_t hi = (uint32_t)(((unsigned long long)ntiles * (qi + 1)) / RG_NQ);
+                if (lo + k < hi) { tile = lo + k; break; }
+#endif
+                qi = (qi + 1) % RG_NQ;
+                ++qtried;
+            }
+            if (tile == 0xFFFFFFFFu) {
+                tiles_left = false;
             } else {
-                // closest-hit lanes and shadow-batch lanes walk the body tables in two
-                // passes; each pass is skipped when no lane of the wave needs it
-                if (mode == MODE_CLOSEST) {
-#ifndef RG_DBG_NO_SEC_TRACE
-                    bool unused = false;
-                    trace_query<F32F, BVH>(a, src, q, false, 0.0, c, unused);
+                if (a.tile_perm) tile = a.tile_perm[tile];  // scheduling order only; every tile is rendered once
+                const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+#ifdef RG_TILE_TIMES
+                cur_tile = tile;
+                t_tile = wall_clock64();
+                t_query = 0;
+                tile_iters = 0;
 #endif
+                const uint32_t x = tx * 8u + (uint32_t)(lane & 7);
+                const uint32_t orow = ty * 8u + (uint32_t)(lane >> 3);
+                bool alive = x < a.width && orow < a.out_rows;
+                const uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
+                oidx = (size_t)orow * a.width + x;
+                if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
+                    a.rgba[oidx] = 0u;
+#ifndef RG_TILE_TIMES
+                    if (a.rgb) { a.rgb[3 * oidx] = 0.0f; a.rgb[3 * oidx + 1] = 0.0f; a.rgb[3 * oidx + 2] = 0.0f; }
+#endif
+                    alive = false;
                 }
-                if (mode == MODE_SHADOW) {
-                    occl = ~occl_full & ((1u << LB) - 1u);  // absent slots count as done
-#ifndef RG_DBG_NO_SHADOW_TRACE
-                    trace_shadow<LB>(a, src, q.o, sb, (1u << LB) - 1u, occl);
-#endif
+                pixel = y * a.width + x;
+                if (alive) {
+                    // ray.rs:37-54 (aspect and fov_adjustment are per-frame constants)
+                    double sx = ((((double)x + 0.5) / (double)a.width) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
+                    double sy = (1.0 - (((double)y + 0.5) / (double)a.height) * 2.0) * a.fov_adjustment;
+                    q.o = v3(0.0, 0.0, 0.0);
+                    q.d = normalize(v3(sx, sy, -1.0));
+                    n_prim++;
+                    closest_init(c);
+                    trace_primary<F32F, BVH>(a, src, q.d, c);
+                    mode = MODE_CLOSEST;
+                    qdepth = 0;
+                    task = -1;
+                    have_result = true;
+                }
+                continue;
+            }
+        }
+        if constexpr (TASKS) {
+            // idle lanes take subtrees other lanes of the block published
+            const bool idle = mode == MODE_DONE;
+            const unsigned long long want = __ballot(idle);
+            if (want != 0ull && pool_any_pending()) {
+                if (idle) {
+                    const int slot = pool_take((int)__builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u)));
+                    if (slot >= 0) {
+                        const double *r = rg_pool.ray[slot];
+                        q.o = v3(r[0], r[1], r[2]);
+                        q.d = v3(r[3], r[4], r[5]);
+                        qdepth = rg_pool.depth[slot];
+                        pixel = rg_pool.pix[slot];
+                        task = slot;
+                        mode = MODE_CLOSEST;
+                        n_sec++;  // the published reflection ray is traced here
+                    }
                 }
             }
-#ifdef RG_TILE_TIMES
-            t_query += wall_clock64() - t_q0;
-#endif
-            have_result = live;
+        }
+        const bool live = mode != MODE_DONE;
+        const bool wave_live = __any(live);
+        if constexpr (TASKS) {
+            if (wave_live != counted) {  // the block's count of waves holding work (helpers' exit test)
+                if (lane == 0) atomicAdd(&rg_pool.busy, wave_live ? 1 : -1);
+                counted = wave_live;
+            }
+        }
+        if (!wave_live) {
+            if (tiles_left) continue;
+            if constexpr (!TASKS) break;
+            // tiles exhausted: serve the block's tasks until no wave holds work
+            if (!pool_any_pending() && __hip_atomic_load(&rg_pool.busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                break;
+            __builtin_amdgcn_s_sleep(4);
+            continue;
+        }
+        const bool querying = mode == MODE_CLOSEST || mode == MODE_SHADOW;  // WAIT lanes only poll
+        if (!__any(querying)) {
+            __builtin_amdgcn_s_sleep(2);
+            have_result = mode == MODE_WAIT;
+            continue;
         }
 #ifdef RG_TILE_TIMES
-        if (lane == 0 && a.rgb) {
-            a.rgb[tile] = (float)(wall_clock64() - t_tile) * 0.01f;  // 100 MHz clock
-            a.rgb[ntiles + tile] = (float)tile_iters;
-            a.rgb[2 * ntiles + tile] = (float)(t_tile & 0xFFFFFFull);  // start, 24-bit 100 MHz ticks (exact in f32)
-            a.rgb[3 * ntiles + tile] = (float)t_query * 0.01f;
-#ifdef RG_BVH_STATS
-            a.rgb[4 * ntiles + tile] = (float)(rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][13] - st0_scan) * 0.01f;
-            a.rgb[5 * ntiles + tile] = (float)(rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][12] - st0_trav) * 0.01f;
-            a.rgb[6 * ntiles + tile] = (float)(rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][8] - st0_lanes);
-            a.rgb[7 * ntiles + tile] = (float)(rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][4] - st0_trv);
-            a.rgb[8 * ntiles + tile] = (float)(rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][5] - st0_steps);
+        ++tile_iters;
+        const unsigned long long t_q0 = wall_clock64();
 #endif
+        if (querying) {
+            closest_init(c);
+            occl = 0u;
         }
+        if constexpr (LB == 1) {
+            // one ray per lane, one pass: closest-hit and shadow lanes share the
+            // body loop (best when a wave mixes ray kinds over many bodies)
+            if (querying) {
+                bool o1 = false;
+                Ray r1;
+                r1.o = q.o;
+                r1.d = mode == MODE_SHADOW ? sb.d[0] : q.d;
+                const bool lane_walk = (mode == MODE_SHADOW ? hdepth : qdepth) >= (int)a.lane_min_depth;
+                trace_query<F32F, BVH>(a, src, r1, mode == MODE_SHADOW, sb.ld[0], c, o1, lane_walk);
+                occl = o1 ? 1u : 0u;
+            }
+        } else {
+            // closest-hit lanes and shadow-batch lanes walk the body tables in two
+            // passes; each pass is skipped when no lane of the wave needs it
+            if (mode == MODE_CLOSEST) {
+#ifndef RG_DBG_NO_SEC_TRACE
+                bool unused = false;
+                trace_query<F32F, BVH>(a, src, q, false, 0.0, c, unused);
 #endif
+            }
+            if (mode == MODE_SHADOW) {
+                occl = ~occl_full & ((1u << LB) - 1u);  // absent slots count as done
+#ifndef RG_DBG_NO_SHADOW_TRACE
+                trace_shadow<LB>(a, src, q.o, sb, (1u << LB) - 1u, occl);
+#endif
+            }
+        }
+#ifdef RG_TILE_TIMES
+        t_query += wall_clock64() - t_q0;
+#endif
+        have_result = querying || mode == MODE_WAIT;
     }
+#ifdef RG_TILE_TIMES
+    if (cur_tile != 0xFFFFFFFFu && lane == 0 && a.rgb) {
+        a.rgb[cur_tile] = (float)(wall_clock64() - t_tile) * 0.01f;
+        a.rgb[ntiles + cur_tile] = (float)tile_iters;
+        a.rgb[2 * ntiles + cur_tile] = (float)(t_tile & 0xFFFFFFull);
+        a.rgb[3 * ntiles + cur_tile] = (float)t_query * 0.01f;
+    }
+#endif
 
     RG_STAT(14, RG_CLOCK() - t_kernel);
     RG_STAT(15, 1);
@@ -1737,11 +1959,11 @@ extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scra
 // ---------------------------------------------------------------- launchers
 // One persistent block per CU slot: grid = CUs x (blocks per CU the register
 // and LDS budgets admit), capped by the tiles the frame has.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH>
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
 static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream) {
     static int cus = 0, per_cu = 0;
     static size_t lds_cached = ~(size_t)0;
-    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH>;
+    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH, TASKS>;
     if (cus == 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
@@ -1774,15 +1996,16 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
 #endif
 // RG_HEAVY_SCENE_BODIES and the path decision (rg_heavy_path) live in rg_device.h
 
-template <int MAXD, int WPS, int LB, bool F32F, bool BVH>
+template <int MAXD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
 static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream) {
     // the BVH kernels also hold the static per-wave traversal stacks
-    constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u);
+    constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u) -
+                                (TASKS ? (uint32_t)sizeof(TaskPool) : 0u);
     if (a->lds_total_bytes <= budget)  // whole scene (empty sphere part if n_sph == 0)
-        return launch_one<MAXD, true, true, WPS, LB, F32F, BVH>(a, a->lds_total_bytes, stream);
+        return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS>(a, a->lds_total_bytes, stream);
     if (a->n_sph > 0 && a->lds_hot_bytes <= budget)
-        return launch_one<MAXD, true, false, WPS, LB, F32F, BVH>(a, a->lds_hot_bytes, stream);
-    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH>(a, a->lds_lstack_bytes, stream);
+        return launch_one<MAXD, true, false, WPS, LB, F32F, BVH, TASKS>(a, a->lds_hot_bytes, stream);
+    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH, TASKS>(a, a->lds_lstack_bytes, stream);
 }
 
 #ifndef RG_LIGHT_WPS
@@ -1796,9 +2019,9 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
     // scenes: the body loop dominates and waves mix ray kinds -> one ray per
     // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
     const bool heavy = rg_heavy_path(*a);
-    if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false>(a, stream);
-    if (a->n_nodes > 0) return launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true>(a, stream);
-    return launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false>(a, stream);
+    if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream);
+    if (a->n_nodes > 0) return launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, RG_HEAVY_TASKS>(a, stream);
+    return launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, RG_HEAVY_TASKS>(a, stream);
 }
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {
