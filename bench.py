@@ -150,46 +150,42 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
     slot = rd.slot_rows(H, world, TILE_ROWS)  # equal-size gather slots (last ranks zero-padded)
     out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
-    use_pipe = (world > 1 or args.pipeline) and args.backend == "nccl"
+    F = max(1, args.frames_in_flight)
+    use_pipe = args.backend == "nccl" or world == 1
     gathered = rd.gather_buffers(out, world) if (world > 1 and rank == 0 and not use_pipe) else None
     frame = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if (rank == 0 and not use_pipe) else None
 
     stream = torch.cuda.current_stream(dev)
     sh = C.c_void_p(stream.cuda_stream)
-    events = []          # (start, end) around each timed launch, on the render stream
-    max_events = [0]
 
     def render(stats=None, buf=None):
+        # on the current stream: the frame pipeline's render stream for this frame, or the default
         dst = out if buf is None else buf
-        st = lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(dst.data_ptr()), None, sh,
+        cur = torch.cuda.current_stream(dev)
+        sh_cur = sh if cur == stream else C.c_void_p(cur.cuda_stream)
+        st = lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(dst.data_ptr()), None, sh_cur,
                                        C.byref(stats) if stats is not None else None)
         _abi.check(st, "rg_render_tiles_async")
 
-    def render_timed(buf=None):
-        if len(events) < max_events[0]:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            render(buf=buf)
-            e1.record(stream)
-            events.append((e0, e1))
-        else:
-            render(buf=buf)
-
     def render_tiles(_t):
-        render_timed()
+        render()
         return out
 
-    # N > 1 over RCCL: frames pipelined two deep (the gather and rank 0's
-    # re-interleave of frame k overlap the render of frame k+1; every frame is
-    # complete when the timed region ends).  The gloo rehearsal gathers through
-    # host memory one frame at a time.
+    # Frames in flight (FramePipeline): frame k renders on render stream k % F
+    # into its own buffer; at N > 1 its tiles are gathered to rank 0 over RCCL
+    # and re-interleaved there while the next frames render.  Consecutive
+    # frames' renders overlap: the next frame's blocks take the CUs the current
+    # frame's slowest tiles leave idle.  Every frame is complete (rendered, and
+    # at N > 1 gathered and assembled on rank 0) when the timed region ends.
+    # The gloo rehearsal gathers through host memory one frame at a time.
     pipe = None
     if use_pipe:
-        pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TILE_ROWS, device=dev)
+        pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TILE_ROWS, device=dev, depth=F,
+                                streams=F > 1 and not args.one_render_stream)
 
     def step():
         if pipe is not None:
-            pipe.step(render_timed)
+            pipe.step(lambda part: render(buf=part))
         else:
             rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
 
@@ -215,7 +211,6 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         dist.barrier()
     torch.cuda.synchronize(dev)
 
-    max_events[0] = args.steps
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -225,6 +220,20 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+
+    # Roofline timing: with frames in flight a launch's start-to-end time
+    # includes the CUs it shares with its neighbours, so the kernel time of one
+    # launch is measured on its own: this rank's share, one launch after
+    # another on one stream, HIP events on that stream (rocprofv3 of
+    # `bench.py --frames-in-flight 1` gives the same average: profiles/).
+    events = []
+    for _ in range(max(1, args.roofline_frames)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        render()
+        e1.record(stream)
+        events.append((e0, e1))
+    torch.cuda.synchronize(dev)
     kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / len(events)
 
     tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -249,6 +258,14 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     if rank != 0:
         return None
 
+    if world > 1:
+        parallelism = f"row-tiles x{world} (round-robin 16-row tiles, one RCCL gather per frame to rank 0"
+    else:
+        parallelism = "one GPU (whole frame"
+    if pipe is not None and pipe.streams:
+        parallelism += f", {F} frames in flight on {F} render streams)"
+    else:
+        parallelism += ", frames rendered one after another on one stream)"
     ms_per_step = elapsed * 1e3 / args.steps
     value = rays_per_frame * args.steps / elapsed / 1e6
     my_rays = stats.rays.primary + stats.rays.shadow + stats.rays.secondary
@@ -264,8 +281,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         "data": src,
         "config": {"workload": label, "width": W, "height": H, "max_recursion_depth": scene.max_recursion_depth,
                    "bodies": body_counts, "lights": len(scene.lights), "tile_rows": TILE_ROWS,
-                   "parallelism": f"row-tiles x{world} (round-robin 16-row tiles, RCCL gather to rank 0"
-                   + (", 2 frames in flight)" if pipe is not None else ")")},
+                   "parallelism": parallelism},
         "rays_per_frame": {"primary": rays[0], "shadow": rays[1], "secondary": rays[2], "total": rays_per_frame},
         "roofline": {
             "bound": "valu_fp64",
@@ -276,7 +292,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
             "traffic": traffic,
             "basis": f"reference-equivalent work: {ops_per_ray} FP64 ops per ray (16/sphere, 14/plane, 20/disk, "
                      f"18/aabb; SURVEY.md 8d) x {my_rays} rays per launch / mean rg_render_kernel time (HIP events "
-                     f"on the render stream)" + (
+                     f"around {max(1, args.roofline_frames)} single-stream launches after the timed region)" + (
                          ". The sphere BVH and f32 pre-filter skip most of that work without changing any result, "
                          "so frac > 1 measures the algorithmic saving over the brute-force scan, not hardware "
                          "utilisation (DESIGN.md 4b)" if bvh.enabled else ""),
@@ -316,14 +332,21 @@ def main() -> None:
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo: rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank renders on GPU 0 (use with --backend gloo)")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="rehearsal: run the N>1 frame pipeline (RCCL gather, overlapped re-interleave) at N=1")
+    ap.add_argument("--frames-in-flight", type=int, default=3,
+                    help="frames in flight, each on its own render stream (N>1: their gathers overlap later renders)")
+    ap.add_argument("--one-render-stream", action="store_true",
+                    help="render every frame on one stream (N>1: only the gathers overlap the renders)")
+    ap.add_argument("--roofline-frames", type=int, default=10,
+                    help="single-stream launches timed after the timed region for the roofline's kernel time")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 checks the gathered frame against a 1-rank render, byte for byte")
     args = ap.parse_args()
     # the JSON line is the only thing on stdout: library banners (RCCL prints its
     # version block on stdout when a communicator is created) go to stderr
     json_out = os.fdopen(os.dup(1), "w")
+    # frames in flight need a hardware queue per render stream next to RCCL's
+    # stream and rank 0's re-interleave stream (HIP's default is 4 per process)
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     sys.stdout.flush()
     os.dup2(2, 1)
 
@@ -335,7 +358,7 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.same_device:
         local_rank = 0
-    if world > 1 or args.pipeline:
+    if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", str(rank))

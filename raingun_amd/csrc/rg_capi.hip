@@ -28,6 +28,18 @@ extern "C" size_t rg_tile_order_scratch_words(uint32_t ntiles);
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,
                                       int32_t *body, hipStream_t stream);
 
+// Per-stream launch state (ray counters, tile-queue heads, error word, tile
+// ordering scratch, timing events).  Launches on distinct streams may run
+// concurrently (frames in flight), so they must not share it; launches on one
+// stream are ordered by the stream and reuse it.
+struct rg_launch_ctx {
+    hipStream_t stream = nullptr;
+    unsigned long long *counters = nullptr;  // RG_COUNTER_WORDS words (rg_device.h)
+    uint32_t *tile_cost = nullptr, *tile_perm = nullptr;  // probe/sort scratch (rg_launch_tile_order), order
+    size_t tile_cap = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
 struct rg_scene {
     int device = 0;
     double fov = 90.0;
@@ -59,14 +71,12 @@ struct rg_scene {
     float bvh_obound = 0.0f;
     double bvh_rbound = 0.0, bvh_margin = 0.0, bvh_extent = 0.0;
     rg_bvh_info bvh_info{};
-    unsigned long long *counters = nullptr;  // RG_COUNTER_WORDS words (rg_device.h)
+    mutable std::vector<rg_launch_ctx *> ctxs;  // one per stream used
+    mutable rg_launch_ctx *last = nullptr;       // the context of the latest launch (rg_debug_counters)
 #ifndef RG_TILE_ORDER
 #define RG_TILE_ORDER -1
 #endif
     int tile_order = RG_TILE_ORDER;  // expensive tiles first (rg_kernels.hip "tile ordering"): -1 auto (heavy path), 0, 1
-    mutable uint32_t *tile_cost = nullptr, *tile_perm = nullptr;  // probe/sort scratch (rg_launch_tile_order), order
-    mutable size_t tile_cap = 0;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
 namespace {
@@ -120,11 +130,35 @@ void release(rg_scene *s) {
     (void)hipSetDevice(s->device);
     for (void *p : s->allocations) (void)hipFree(p);
     s->allocations.clear();
-    if (s->tile_cost) (void)hipFree(s->tile_cost);
-    if (s->tile_perm) (void)hipFree(s->tile_perm);
-    if (s->ev0) (void)hipEventDestroy(s->ev0);
-    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    for (rg_launch_ctx *c : s->ctxs) {
+        if (c->counters) (void)hipFree(c->counters);
+        if (c->tile_cost) (void)hipFree(c->tile_cost);
+        if (c->tile_perm) (void)hipFree(c->tile_perm);
+        if (c->ev0) (void)hipEventDestroy(c->ev0);
+        if (c->ev1) (void)hipEventDestroy(c->ev1);
+        delete c;
+    }
     delete s;
+}
+
+// The launch context of `stream`, created on first use (nullptr: out of memory / device error).
+rg_launch_ctx *ctx_for(const rg_scene *s, hipStream_t stream) {
+    for (rg_launch_ctx *c : s->ctxs)
+        if (c->stream == stream) return c;
+    rg_launch_ctx *c = new (std::nothrow) rg_launch_ctx();
+    if (!c) return nullptr;
+    c->stream = stream;
+    void *p = nullptr;
+    if (!ok(hipMalloc(&p, RG_COUNTER_WORDS * sizeof(unsigned long long)))) { delete c; return nullptr; }
+    c->counters = static_cast<unsigned long long *>(p);
+    if (!ok(hipEventCreate(&c->ev0)) || !ok(hipEventCreate(&c->ev1))) {
+        (void)hipFree(c->counters);
+        if (c->ev0) (void)hipEventDestroy(c->ev0);
+        delete c;
+        return nullptr;
+    }
+    s->ctxs.push_back(c);
+    return c;
 }
 
 RgKernelArgs make_args(const rg_scene *s) {
@@ -189,7 +223,6 @@ RgKernelArgs make_args(const rg_scene *s) {
     a.def[2] = s->def[2];
     a.max_depth = s->max_depth;
     a.fov_adjustment = fov_adjustment(s->fov);
-    a.counters = s->counters;
     return a;
 }
 
@@ -408,12 +441,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         texs[i].texels = dp;
     }
     if (st == RG_OK) st = upload(s, &s->texs, texs.data(), texs.size());
-    if (st == RG_OK) {
-        void *p = nullptr;
-        if (!ok(hipMalloc(&p, RG_COUNTER_WORDS * sizeof(unsigned long long)))) st = RG_ERR_OUT_OF_MEMORY;
-        else { s->allocations.push_back(p); s->counters = static_cast<unsigned long long *>(p); }
-    }
-    if (st == RG_OK && (!ok(hipEventCreate(&s->ev0)) || !ok(hipEventCreate(&s->ev1)))) st = RG_ERR_DEVICE;
+    if (st == RG_OK && !(s->last = ctx_for(s, nullptr))) st = RG_ERR_OUT_OF_MEMORY;  // default-stream context
     if (st != RG_OK) { release(s); return st; }
     *out = s;
     return RG_OK;
@@ -437,7 +465,11 @@ rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t heig
         return RG_ERR_INVALID_ARGUMENT;  // the reference's u32 pixel index (rendering.rs:27)
     if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
     hipStream_t st = static_cast<hipStream_t>(stream);
+    rg_launch_ctx *cx = ctx_for(s, st);
+    if (!cx) return RG_ERR_OUT_OF_MEMORY;
+    s->last = cx;
     RgKernelArgs a = make_args(s);
+    a.counters = cx->counters;
     a.width = width;
     a.height = height;
     a.tile_rows = tiling->tile_rows;
@@ -447,32 +479,32 @@ rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t heig
     a.aspect = (double)width / (double)height;
     a.rgba = reinterpret_cast<uint32_t *>(rgba_dev);
     a.rgb = rgb_dev;
-    if (!ok(hipMemsetAsync(s->counters, 0, RG_COUNTER_WORDS * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
-    if (stats && !ok(hipEventRecord(s->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
+    if (!ok(hipMemsetAsync(cx->counters, 0, RG_COUNTER_WORDS * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
+    if (stats && !ok(hipEventRecord(cx->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
     if (s->tile_order == 1 || (s->tile_order < 0 && rg_heavy_path(a))) {
         const size_t ntiles = (size_t)((width + 7u) / 8u) * ((out_rows + 7u) / 8u);
-        if (ntiles > s->tile_cap) {
-            if (s->tile_cost) (void)hipFree(s->tile_cost);
-            if (s->tile_perm) (void)hipFree(s->tile_perm);
-            s->tile_cost = s->tile_perm = nullptr;
-            s->tile_cap = 0;
-            if (!ok(hipMalloc(&s->tile_cost, rg_tile_order_scratch_words((uint32_t)ntiles) * 4)) ||
-                !ok(hipMalloc(&s->tile_perm, ntiles * 4)))
+        if (ntiles > cx->tile_cap) {
+            if (cx->tile_cost) (void)hipFree(cx->tile_cost);
+            if (cx->tile_perm) (void)hipFree(cx->tile_perm);
+            cx->tile_cost = cx->tile_perm = nullptr;
+            cx->tile_cap = 0;
+            if (!ok(hipMalloc(&cx->tile_cost, rg_tile_order_scratch_words((uint32_t)ntiles) * 4)) ||
+                !ok(hipMalloc(&cx->tile_perm, ntiles * 4)))
                 return RG_ERR_OUT_OF_MEMORY;
-            s->tile_cap = ntiles;
+            cx->tile_cap = ntiles;
         }
-        if (!ok(rg_launch_tile_order(&a, s->tile_cost, s->tile_perm, st))) return RG_ERR_DEVICE;
-        a.tile_perm = s->tile_perm;
+        if (!ok(rg_launch_tile_order(&a, cx->tile_cost, cx->tile_perm, st))) return RG_ERR_DEVICE;
+        a.tile_perm = cx->tile_perm;
     }
     if (out_rows == 0) return RG_OK;
     if (!ok(rg_launch_render(&a, frames_needed(s->max_depth), st))) return RG_ERR_DEVICE;
     if (!stats) return RG_OK;
-    if (!ok(hipEventRecord(s->ev1, st))) return RG_ERR_DEVICE;
+    if (!ok(hipEventRecord(cx->ev1, st))) return RG_ERR_DEVICE;
     unsigned long long c[4];
-    if (!ok(hipMemcpyAsync(c, s->counters, sizeof c, hipMemcpyDeviceToHost, st))) return RG_ERR_DEVICE;
+    if (!ok(hipMemcpyAsync(c, cx->counters, sizeof c, hipMemcpyDeviceToHost, st))) return RG_ERR_DEVICE;
     if (!ok(hipStreamSynchronize(st))) return RG_ERR_DEVICE;
     float ms = 0.0f;
-    (void)hipEventElapsedTime(&ms, s->ev0, s->ev1);
+    (void)hipEventElapsedTime(&ms, cx->ev0, cx->ev1);
     stats->rays.primary = c[0];
     stats->rays.shadow = c[1];
     stats->rays.secondary = c[2];
@@ -613,7 +645,9 @@ rg_status rg_debug_set_tile_order(rg_scene *s, int32_t mode) {
 rg_status rg_debug_counters(const rg_scene *s, uint64_t out[16]) {
     if (!s || !out) return RG_ERR_INVALID_ARGUMENT;
     if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
-    if (!ok(hipMemcpy(out, s->counters, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost))) return RG_ERR_DEVICE;
+    if (!ok(hipStreamSynchronize(s->last->stream)) ||
+        !ok(hipMemcpy(out, s->last->counters, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost)))
+        return RG_ERR_DEVICE;
     return RG_OK;
 }
 
@@ -626,14 +660,17 @@ rg_status rg_trace(const rg_scene *s, const double *rays, uint32_t n, double *di
     if (!ok(hipMalloc(&d_rays, (size_t)n * 48)) || !ok(hipMalloc(&d_dist, (size_t)n * 8)) ||
         !ok(hipMalloc(&d_body, (size_t)n * 4)))
         st = RG_ERR_OUT_OF_MEMORY;
+    rg_launch_ctx *cx = ctx_for(s, nullptr);
+    if (!cx) st = RG_ERR_OUT_OF_MEMORY;
     RgKernelArgs a = make_args(s);
     unsigned long long c[4] = {0, 0, 0, 0};
+    if (st == RG_OK) { s->last = cx; a.counters = cx->counters; }
     if (st == RG_OK && (!ok(hipMemcpy(d_rays, rays, (size_t)n * 48, hipMemcpyHostToDevice)) ||
-                        !ok(hipMemset(s->counters, 0, sizeof c)) ||
+                        !ok(hipMemset(cx->counters, 0, sizeof c)) ||
                         !ok(rg_launch_trace(&a, (const double *)d_rays, n, (double *)d_dist, (int32_t *)d_body, nullptr)) ||
                         !ok(hipMemcpy(dist, d_dist, (size_t)n * 8, hipMemcpyDeviceToHost)) ||
                         !ok(hipMemcpy(body, d_body, (size_t)n * 4, hipMemcpyDeviceToHost)) ||
-                        !ok(hipMemcpy(c, s->counters, sizeof c, hipMemcpyDeviceToHost))))
+                        !ok(hipMemcpy(c, cx->counters, sizeof c, hipMemcpyDeviceToHost))))
         st = RG_ERR_DEVICE;
     if (d_rays) (void)hipFree(d_rays);
     if (d_dist) (void)hipFree(d_dist);

@@ -143,10 +143,17 @@ class FramePipeline:
     its previous frame's gather (and, on rank 0, re-interleave) finished.
     `flush()` completes every frame in flight.  On CPU tensors (gloo) the
     same sequence runs synchronously, and `on_frame(k, frame)` (rank 0) sees
-    each assembled frame.  One collective per frame: the gather."""
+    each assembled frame.  One collective per frame: the gather.
+
+    `streams=True` (CUDA) renders frame k on render stream k % depth, so the
+    renders of consecutive frames may also overlap: the next frame's blocks
+    take the CUs the current frame's slowest tiles leave idle (a rank's share
+    of a frame is tail-bound: its makespan is set by its slowest 8x8 tiles,
+    not by its average work).  The library keeps separate launch state per
+    stream, so the two launches never share counters or tile queues."""
 
     def __init__(self, part_shape, height: int, rank: int, world: int, tile_rows: int = TILE_ROWS,
-                 device=None, depth: int = 2, group=None, on_frame=None):
+                 device=None, depth: int = 2, group=None, on_frame=None, streams: bool = False):
         import torch
 
         self.H, self.rank, self.world, self.T, self.group = height, rank, world, tile_rows, group
@@ -157,15 +164,18 @@ class FramePipeline:
         self.works = [None] * depth
         self.frames = [None] * depth          # frame index held by each buffer
         self.asm_done = [None] * depth        # rank 0, CUDA: re-interleave finished (event)
-        if rank == 0:
+        if rank == 0 and world > 1:
             self.gathered = [torch.empty((world,) + tuple(part_shape), **kw) for _ in range(depth)]
             self.frame_padded = torch.empty((world * part_shape[0],) + tuple(part_shape[1:]), **kw)
             self.side = torch.cuda.Stream(device) if self.cuda else None
+        self.streams = [torch.cuda.Stream(device) for _ in range(depth)] if (self.cuda and streams) else None
         self.k = 0
 
     @property
     def frame(self):
         """Rank 0's latest assembled frame (image order, `height` rows)."""
+        if self.world == 1:  # one rank: its part is the frame (no gather)
+            return self.parts[(self.k - 1) % self.depth][:self.H]
         return self.frame_padded[:self.H]
 
     def _retire(self, b):
@@ -183,14 +193,34 @@ class FramePipeline:
         self.works[b] = None
 
     def step(self, render):
-        """Enqueue one frame: `render(part)` writes this rank's tiles into `part`."""
+        """Enqueue one frame: `render(part)` writes this rank's tiles into `part`
+        on the current stream (render stream k % depth with `streams`)."""
+        import contextlib
+
+        import torch
+
+        b = self.k % self.depth
+        if self.streams is None:
+            self._step(render, b)
+        else:
+            s = self.streams[b]
+            s.wait_stream(torch.cuda.current_stream())  # work the caller enqueued before this frame
+            with torch.cuda.stream(s):
+                self._step(render, b)
+
+    def _step(self, render, b):
         import torch
         import torch.distributed as dist
 
-        b = self.k % self.depth
         self._retire(b)
         part = self.parts[b]
         render(part)
+        if self.world == 1:  # nothing to gather: the part is the frame
+            self.frames[b] = self.k
+            if not self.cuda and self.on_frame is not None:
+                self.on_frame(self.k, self.frame_of(b))
+            self.k += 1
+            return
         bufs = list(self.gathered[b].unbind(0)) if self.rank == 0 else None
         work = dist.gather(part, bufs, dst=0, group=self.group, async_op=True)
         self.works[b], self.frames[b] = work, self.k
@@ -211,7 +241,15 @@ class FramePipeline:
             work.wait()
         self.k += 1
 
+    def frame_of(self, b):
+        return self.parts[b][:self.H]
+
     def flush(self):
         """Complete every frame in flight (the current stream then holds them all)."""
+        import torch
+
         for b in range(self.depth):
             self._retire(b)
+        if self.streams is not None:  # the renders (one rank: nothing else follows them)
+            for s in self.streams:
+                torch.cuda.current_stream().wait_stream(s)

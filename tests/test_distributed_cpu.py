@@ -124,3 +124,19 @@ def test_assemble_into_matches_assemble():
     fp = torch.empty((world * slot, W, 4), dtype=torch.uint8)
     rd.assemble_into(fp, g, world, T)
     assert torch.equal(fp[:H], rd.assemble(list(g.unbind(0)), H, world, T))
+
+
+def test_frame_pipeline_single_rank_needs_no_collective():
+    """At N = 1 the pipeline only rotates render buffers (no process group, no
+    gather): frame k is the part it rendered, delivered in order."""
+    H, W, T, K, depth = 40, 6, 16, 7, 3
+    slot = rd.slot_rows(H, 1, T)
+    got = {}
+    pipe = rd.FramePipeline((slot, W, 4), H, 0, 1, T, depth=depth, on_frame=lambda k, f: got.__setitem__(k, f.clone()))
+    for k in range(K):
+        pipe.step(lambda part, k=k: part.fill_(k))
+        assert pipe.frame.shape == (H, W, 4) and int(pipe.frame[0, 0, 0]) == k
+    pipe.flush()
+    assert sorted(got) == list(range(K))
+    for k in range(K):
+        assert bool((got[k] == k).all())

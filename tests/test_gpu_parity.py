@@ -282,3 +282,37 @@ def test_tile_order_changes_nothing(oracle_lib, example_scenes, scene_kind):
         assert np.array_equal(rgba, o_rgba) and np.array_equal(part, o_part)
         assert float(np.abs(rgb - o_rgb).max()) <= RGB_TOL
         assert st.rays.as_dict() == o_counts
+
+
+@pytest.mark.parametrize("scene_kind", ["synth200", "test1"])
+def test_frames_in_flight_on_concurrent_streams(oracle_lib, example_scenes, scene_kind):
+    """Frames in flight (bench.py, FramePipeline): launches of one scene on
+    distinct streams run concurrently, each with its own launch state (ray
+    counters, tile queues, tile-order scratch).  Every part must still equal
+    the CPU restatement, and a counted launch afterwards must count exactly."""
+    import ctypes as C
+
+    import torch
+
+    scene = synthetic_scene(200, 2, 5) if scene_kind == "synth200" else example_scenes[scene_kind]
+    w, h, T, F = 320, 180, 16, 3
+    ds = DeviceScene(scene)
+    lib = _abi.lib()
+    streams = [torch.cuda.Stream() for _ in range(F)]
+    tilings = [_abi.rg_tiling(T, F, i) for i in range(F)]
+    rows = [lib.rg_tiling_rows(h, C.byref(t)) for t in tilings]
+    bufs = [[torch.full((rows[i], w, 4), 7, dtype=torch.uint8, device="cuda") for _ in range(2)] for i in range(F)]
+    for rnd in range(4):  # several rounds: each stream's launches queue behind the others' in flight
+        for i in range(F):
+            b = bufs[i][rnd % 2]
+            _abi.check(lib.rg_render_tiles_async(ds.handle, w, h, C.byref(tilings[i]), C.c_void_p(b.data_ptr()),
+                                                 None, C.c_void_p(streams[i].cuda_stream), None))
+    torch.cuda.synchronize()
+    for i in range(F):
+        _, o_part, _, _, _ = oracle_lib.render(SceneDesc(scene), w, h, T, F, i)
+        for b in bufs[i]:
+            assert np.array_equal(b.cpu().numpy(), o_part), f"stream {i}"
+    st = _abi.rg_stats()
+    ds.render_tiles(w, h, stats=st)
+    ds.close()
+    assert st.rays.as_dict() == oracle_lib.render(SceneDesc(scene), w, h)[3]
