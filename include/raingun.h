@@ -174,7 +174,11 @@ rg_status rg_render_image(const rg_scene *scene, uint32_t width, uint32_t height
  * (a hipStream_t; NULL = null stream).  `rgb_dev` (nullable, device) receives
  * the pre-quantisation f32 RGB (3 floats per pixel, same packing) for float
  * parity checks.  Asynchronous unless `stats` is non-NULL, in which case the
- * call synchronises `stream` and fills ray counts, kernel time and errors. */
+ * call synchronises `stream` and fills ray counts, kernel time and errors.
+ * Launches of one scene on DISTINCT streams may be in flight together (frames
+ * in flight): each stream has its own launch state (ray counters, tile queue,
+ * error word), created on the stream's first use.  Calls on one scene must
+ * come from one host thread at a time. */
 rg_status rg_render_tiles_async(const rg_scene *scene, uint32_t width, uint32_t height,
                                 const rg_tiling *tiling, uint8_t *rgba_dev, float *rgb_dev,
                                 void *stream, rg_stats *stats);
