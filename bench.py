@@ -181,7 +181,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     pipe = None
     if use_pipe:
         pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TILE_ROWS, device=dev, depth=F,
-                                streams=F > 1 and not args.one_render_stream)
+                                streams=F > 1 and not args.one_render_stream, gather=world > 1 or args.rccl_rehearsal)
 
     def step():
         if pipe is not None:
@@ -338,6 +338,8 @@ def main() -> None:
                     help="render every frame on one stream (N>1: only the gathers overlap the renders)")
     ap.add_argument("--roofline-frames", type=int, default=10,
                     help="single-stream launches timed after the timed region for the roofline's kernel time")
+    ap.add_argument("--rccl-rehearsal", action="store_true",
+                    help="N=1: run the N>1 path anyway (RCCL process group, per-frame gather, re-interleave)")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 checks the gathered frame against a 1-rank render, byte for byte")
     args = ap.parse_args()
@@ -358,7 +360,7 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.same_device:
         local_rank = 0
-    if world > 1:
+    if world > 1 or args.rccl_rehearsal:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", str(rank))

@@ -153,18 +153,20 @@ class FramePipeline:
     stream, so the two launches never share counters or tile queues."""
 
     def __init__(self, part_shape, height: int, rank: int, world: int, tile_rows: int = TILE_ROWS,
-                 device=None, depth: int = 2, group=None, on_frame=None, streams: bool = False):
+                 device=None, depth: int = 2, group=None, on_frame=None, streams: bool = False,
+                 gather: bool = None):
         import torch
 
         self.H, self.rank, self.world, self.T, self.group = height, rank, world, tile_rows, group
         self.depth, self.on_frame = depth, on_frame
+        self.gather = world > 1 if gather is None else gather  # gather=True at world 1: rehearse the collective path
         self.cuda = device is not None and torch.device(device).type == "cuda"
         kw = dict(dtype=torch.uint8, device=device)
         self.parts = [torch.zeros(part_shape, **kw) for _ in range(depth)]
         self.works = [None] * depth
         self.frames = [None] * depth          # frame index held by each buffer
         self.asm_done = [None] * depth        # rank 0, CUDA: re-interleave finished (event)
-        if rank == 0 and world > 1:
+        if rank == 0 and self.gather:
             self.gathered = [torch.empty((world,) + tuple(part_shape), **kw) for _ in range(depth)]
             self.frame_padded = torch.empty((world * part_shape[0],) + tuple(part_shape[1:]), **kw)
             self.side = torch.cuda.Stream(device) if self.cuda else None
@@ -174,7 +176,7 @@ class FramePipeline:
     @property
     def frame(self):
         """Rank 0's latest assembled frame (image order, `height` rows)."""
-        if self.world == 1:  # one rank: its part is the frame (no gather)
+        if not self.gather:  # one rank: its part is the frame
             return self.parts[(self.k - 1) % self.depth][:self.H]
         return self.frame_padded[:self.H]
 
@@ -215,7 +217,7 @@ class FramePipeline:
         self._retire(b)
         part = self.parts[b]
         render(part)
-        if self.world == 1:  # nothing to gather: the part is the frame
+        if not self.gather:  # one rank: nothing to gather, the part is the frame
             self.frames[b] = self.k
             if not self.cuda and self.on_frame is not None:
                 self.on_frame(self.k, self.frame_of(b))
