@@ -150,7 +150,10 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
     slot = rd.slot_rows(H, world, TILE_ROWS)  # equal-size gather slots (last ranks zero-padded)
     out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
-    F = max(1, args.frames_in_flight)
+    # frames in flight: 3 at N = 1 (3 render streams + the null stream fill
+    # HIP's 4 default queues), 4 at N > 1 (8 queues, see main; a rank's share
+    # is more tail-bound: profiles/r01/frames_in_flight_overlap_probe.json)
+    F = args.frames_in_flight if args.frames_in_flight > 0 else (4 if world > 1 else 3)
     use_pipe = args.backend == "nccl" or world == 1
     gathered = rd.gather_buffers(out, world) if (world > 1 and rank == 0 and not use_pipe) else None
     frame = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if (rank == 0 and not use_pipe) else None
@@ -332,8 +335,9 @@ def main() -> None:
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo: rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank renders on GPU 0 (use with --backend gloo)")
-    ap.add_argument("--frames-in-flight", type=int, default=3,
-                    help="frames in flight, each on its own render stream (N>1: their gathers overlap later renders)")
+    ap.add_argument("--frames-in-flight", type=int, default=0,
+                    help="frames in flight, each on its own render stream (N>1: their gathers overlap later renders); "
+                         "0 = 3 at N=1, 4 at N>1")
     ap.add_argument("--one-render-stream", action="store_true",
                     help="render every frame on one stream (N>1: only the gathers overlap the renders)")
     ap.add_argument("--roofline-frames", type=int, default=10,
