@@ -168,8 +168,15 @@ class FramePipeline:
         self.asm_done = [None] * depth        # rank 0, CUDA: re-interleave finished (event)
         if rank == 0 and self.gather:
             self.gathered = [torch.empty((world,) + tuple(part_shape), **kw) for _ in range(depth)]
+            self.recv = [list(g.unbind(0)) for g in self.gathered]
             self.frame_padded = torch.empty((world * part_shape[0],) + tuple(part_shape[1:]), **kw)
             self.side = torch.cuda.Stream(device) if self.cuda else None
+            if self.cuda:  # assemble_into's strided copy, its views built once
+                tpr = part_shape[0] // tile_rows
+                self.asm_src = [g.reshape((world, tpr, tile_rows) + tuple(part_shape[1:])).transpose(0, 1)
+                                for g in self.gathered]
+                self.asm_dst = self.frame_padded.view((tpr, world, tile_rows) + tuple(part_shape[1:]))
+                self.asm_done = [torch.cuda.Event() for _ in range(depth)]
         self.streams = [torch.cuda.Stream(device) for _ in range(depth)] if (self.cuda and streams) else None
         self.k = 0
 
@@ -197,17 +204,16 @@ class FramePipeline:
     def step(self, render):
         """Enqueue one frame: `render(part)` writes this rank's tiles into `part`
         on the current stream (render stream k % depth with `streams`)."""
-        import contextlib
-
         import torch
 
         b = self.k % self.depth
         if self.streams is None:
             self._step(render, b)
         else:
-            s = self.streams[b]
-            s.wait_stream(torch.cuda.current_stream())  # work the caller enqueued before this frame
-            with torch.cuda.stream(s):
+            # frame k depends only on frame k - depth (its buffer) and the scene:
+            # the render stream does not wait for the caller's stream (host cost
+            # per frame is the N > 1 bound at small shares: scripts/host_overhead_probe.py)
+            with torch.cuda.stream(self.streams[b]):
                 self._step(render, b)
 
     def _step(self, render, b):
@@ -223,17 +229,14 @@ class FramePipeline:
                 self.on_frame(self.k, self.frame_of(b))
             self.k += 1
             return
-        bufs = list(self.gathered[b].unbind(0)) if self.rank == 0 else None
-        work = dist.gather(part, bufs, dst=0, group=self.group, async_op=True)
+        work = dist.gather(part, self.recv[b] if self.rank == 0 else None, dst=0, group=self.group, async_op=True)
         self.works[b], self.frames[b] = work, self.k
         if self.rank == 0:
             if self.cuda:
                 with torch.cuda.stream(self.side):
                     work.wait()  # side stream waits for the gather
-                    assemble_into(self.frame_padded, self.gathered[b], self.world, self.T)
-                    ev = torch.cuda.Event()
-                    ev.record(self.side)
-                    self.asm_done[b] = ev
+                    self.asm_dst.copy_(self.asm_src[b])  # re-interleave (assemble_into, views made once)
+                    self.asm_done[b].record(self.side)
             else:
                 work.wait()
                 assemble_into(self.frame_padded, self.gathered[b], self.world, self.T)
