@@ -481,7 +481,9 @@ __device__ __forceinline__ void leaf_query(const RgKernelArgs &a, const Src &src
     }
 }
 
-// KIND 0: primary ray (o = 0); 1: closest hit; 2: any hit with t <= ld.
+// KIND 0: primary ray (o = 0); 1: a query, per lane closest hit or (`shadow`)
+// any hit with t <= ld -- closest-hit and shadow lanes of a wave share ONE walk
+// instead of running one walk per kind one after the other.
 // Called by the lanes that take the BVH (exec mask); `need` drops for a
 // shadow lane at its first occluder.  The box tests start at o + t0s d
 // (t0s > 0 only for far origins, rg_bvh_classify) and prune against
@@ -489,15 +491,15 @@ __device__ __forceinline__ void leaf_query(const RgKernelArgs &a, const Src &src
 __device__ __forceinline__ float bvh_bound(double v) { return v <= 0.0 ? 0.0f : rg_f32_up(v); }
 
 template <int KIND, bool GROW = false, class Src>
-__device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &src, V3 o, V3 d, double ld, double t0s,
-                                            Closest &c, bool &occl, bool &need, float grow = 0.0f) {
+__device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &src, V3 o, V3 d, bool shadow, double ld,
+                                            double t0s, Closest &c, bool &occl, bool &need, float grow = 0.0f) {
     int *stack = rg_bvh_stack[threadIdx.x >> 6];
     const V3 ob = t0s > 0.0 ? add(o, scl(d, t0s)) : o;
     const RayB rb = rg_make_rayb(ob.x, ob.y, ob.z, d.x, d.y, d.z);
     RayF rf;
     const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
     if constexpr (KIND != 0) rf = make_rayf(o, d);
-    const float tld = KIND == 2 ? bvh_bound(ld - t0s) : 0.0f;
+    const float tld = shadow ? bvh_bound(ld - t0s) : 0.0f;
     const int lane = (int)(threadIdx.x & 63u);
     const bool writer = lane == wave_uniform(lane);
     int sp = 0;
@@ -509,7 +511,7 @@ __device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &sr
         RG_STAT(5, 1);
         const RgBvhNode N = src.getn(node);
         const int nch = wave_uniform(N.nchild);
-        const float tb = KIND == 2 ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
+        const float tb = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
         int next = -1;
         float next_key = 0.0f;
 #pragma unroll
@@ -524,7 +526,7 @@ __device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &sr
                         RG_STAT(6, 1);
                         if (h) {
                             if constexpr (KIND == 0) leaf_primary(a, src, first, count, d, dx, dy, dz, c);
-                            else leaf_query(a, src, first, count, o, d, rf, KIND == 2, ld, c, occl, need);
+                            else leaf_query(a, src, first, count, o, d, rf, shadow, ld, c, occl, need);
                         }
                     } else {
                         const float key = wave_uniform_f(h ? tn : __builtin_huge_valf());
@@ -542,8 +544,8 @@ __device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &sr
                 }
             }
         }
-        if constexpr (KIND == 2) {
-            if (!__any(need)) break;
+        if constexpr (KIND != 0) {
+            if (!__any(need)) break;  // every shadow lane occluded (closest-hit lanes keep `need`)
         }
         if (next >= 0) {
             node = next;
@@ -581,9 +583,9 @@ __device__ __forceinline__ void cswap(uint32_t &x, uint32_t &y) {
     y = hi;
 }
 
-template <int KIND, class Src>
-__device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, V3 o, V3 d, double ld, double t0s,
-                                         Closest &c, bool &occl, bool &need) {
+template <class Src>
+__device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, V3 o, V3 d, bool shadow, double ld,
+                                         double t0s, Closest &c, bool &occl, bool &need) {
     uint32_t *stk = reinterpret_cast<uint32_t *>(rg_dyn_smem) + threadIdx.x;  // entry e at stk[e * blockDim.x]
     const uint32_t stride = blockDim.x;
     const int cap = a.lane_stack;
@@ -591,7 +593,7 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
     const V3 ob = t0s > 0.0 ? add(o, scl(d, t0s)) : o;
     const RayB rb = rg_make_rayb(ob.x, ob.y, ob.z, d.x, d.y, d.z);
     const RayF rf = make_rayf(o, d);
-    const float tld = KIND == 2 ? bvh_bound(ld - t0s) : 0.0f;
+    const float tld = shadow ? bvh_bound(ld - t0s) : 0.0f;
     int node = 0, sp = 0;
     RG_STAT(4, 1);
     RG_STAT(7, RG_LANES(1));
@@ -602,7 +604,7 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
         RG_STAT(5, 1);
         if (act) {
             const RgBvhNode N = src.getn(node);
-            const float tb = KIND == 2 ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
+            const float tb = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
             uint32_t e0 = ~0u, e1 = ~0u, e2 = ~0u, e3 = ~0u;
             int l0 = 0, l1 = 0, l2 = 0, l3 = 0, nl = 0;  // hit leaf children, in child order
 #pragma unroll
@@ -629,7 +631,7 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             // test, looped max-over-lanes times, instead of one per child slot
             while (nl > 0 && need) {
                 const int v = ~l0;
-                leaf_query(a, src, v >> 3, (v & 7) + 1, o, d, rf, KIND == 2, ld, c, occl, need);
+                leaf_query(a, src, v >> 3, (v & 7) + 1, o, d, rf, shadow, ld, c, occl, need);
                 l0 = l1; l1 = l2; l2 = l3;
                 --nl;
             }
@@ -638,14 +640,14 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             if (e3 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e3;
             if (e2 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e2;
             if (e1 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e1;
-            const float tbn = KIND == 2 ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
-            if (e0 != ~0u && (KIND == 2 || !(lane_key_t(e0) > tbn))) {
+            const float tbn = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
+            if (e0 != ~0u && (shadow || !(lane_key_t(e0) > tbn))) {
                 node = (int)(e0 & mask);
             } else {
                 node = -1;
                 while (sp > 0 && need) {
                     const uint32_t e = stk[(uint32_t)(--sp) * stride];
-                    if (KIND == 2 || !(lane_key_t(e) > tbn)) {
+                    if (shadow || !(lane_key_t(e) > tbn)) {
                         node = (int)(e & mask);
                         break;
                     }
@@ -692,7 +694,7 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
         }
         if (ok) {
             bool need = true, unused = false;
-            bvh_spheres<0>(a, src, o, d, 0.0, 0.0, c, unused, need);
+            bvh_spheres<0>(a, src, o, d, false, 0.0, 0.0, c, unused, need);
         }
     }
 }
@@ -777,16 +779,13 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
         const bool grown = ok && grow > 0.0f;  // far rays: boxes grown in the slab test
         const bool per_lane = ok && !grown && lane_walk && a.lane_stack > 0;  // incoherent rays
         if (per_lane) {
-            if (shadow) bvh_lane<2>(a, src, o, d, ld, t0s, c, occl, need);
-            else bvh_lane<1>(a, src, o, d, ld, t0s, c, occl, need);
+            bvh_lane(a, src, o, d, shadow, ld, t0s, c, occl, need);
         }
         if (ok && !grown && !per_lane) {
-            if (shadow) bvh_spheres<2>(a, src, o, d, ld, t0s, c, occl, need);
-            else bvh_spheres<1>(a, src, o, d, ld, t0s, c, occl, need);
+            bvh_spheres<1>(a, src, o, d, shadow, ld, t0s, c, occl, need);
         }
         if (grown) {
-            if (shadow) bvh_spheres<2, true>(a, src, o, d, ld, t0s, c, occl, need, grow);
-            else bvh_spheres<1, true>(a, src, o, d, ld, t0s, c, occl, need, grow);
+            bvh_spheres<1, true>(a, src, o, d, shadow, ld, t0s, c, occl, need, grow);
         }
     }
 }
