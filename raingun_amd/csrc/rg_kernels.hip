@@ -777,7 +777,16 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
             RG_STAT(13, RG_CLOCK() - t0);
         }
         const bool grown = ok && grow > 0.0f;  // far rays: boxes grown in the slab test
+#ifndef RG_MIX_LANE
+#define RG_MIX_LANE 1
+#endif
+#if RG_MIX_LANE
+        // one walk kind per wave: if any lane's ray is incoherent, every near lane walks per lane
+        // (a mixed wave would otherwise run the per-lane walk and then the wave walk)
+        const bool per_lane = ok && !grown && a.lane_stack > 0 && __any(ok && !grown && lane_walk);
+#else
         const bool per_lane = ok && !grown && lane_walk && a.lane_stack > 0;  // incoherent rays
+#endif
         if (per_lane) {
             bvh_lane(a, src, o, d, shadow, ld, t0s, c, occl, need);
         }
