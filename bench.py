@@ -150,9 +150,9 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
     slot = rd.slot_rows(H, world, TILE_ROWS)  # equal-size gather slots (last ranks zero-padded)
     out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
-    # frames in flight: 3 at N = 1 (3 render streams + the null stream fill
-    # HIP's 4 default queues), 4 at N > 1 (8 queues, see main; a rank's share
-    # is more tail-bound: profiles/r01/frames_in_flight_overlap_probe.json)
+    # frames in flight, each on its own render stream and hardware queue (8 per
+    # process, see main): 3 at N = 1, 4 at N > 1, where a rank's share is more
+    # tail-bound (profiles/r01/frames_in_flight_overlap_probe*.json)
     F = args.frames_in_flight if args.frames_in_flight > 0 else (4 if world > 1 else 3)
     use_pipe = args.backend == "nccl" or world == 1
     gathered = rd.gather_buffers(out, world) if (world > 1 and rank == 0 and not use_pipe) else None
@@ -324,8 +324,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="test1", help="test1 | test3 | synth<N>")
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)

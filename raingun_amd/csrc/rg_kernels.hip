@@ -1967,8 +1967,19 @@ extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scra
 // ---------------------------------------------------------------- launchers
 // One persistent block per CU slot: grid = CUs x (blocks per CU the register
 // and LDS budgets admit), capped by the tiles the frame has.
+#ifndef RG_LIGHT_BLOCK_WAVES
+#define RG_LIGHT_BLOCK_WAVES 1  // light path: waves per block (blocks retire wave by wave)
+#endif
 template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
 static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream) {
+    // Block size.  The heavy path shares one LDS copy of the scene (and the
+    // BVH stacks / task pool) among the CU's 4*WPS waves: one block per CU.
+    // The light path's scene is a few KB, so it runs small blocks, each with
+    // its own copy: a block then holds its CU slot only while ITS waves work,
+    // and with frames in flight the next frame's blocks take the slots of
+    // waves that finished (a 4*WPS-wave block would keep the CU until its
+    // slowest wave -- one refractive tile -- is done).
+    constexpr int threads = (!BVH && !TASKS) ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS;
     static int cus = 0, per_cu = 0;
     static size_t lds_cached = ~(size_t)0;
     auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH, TASKS>;
@@ -1981,18 +1992,18 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
         if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return hipErrorInvalidValue;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256 * WPS, lds) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess)
             return hipErrorInvalidValue;
         if (per_cu < 1) return hipErrorInvalidConfiguration;
         lds_cached = lds;
     }
     const unsigned long long tiles = (unsigned long long)((a->width + 7) / 8) * ((a->out_rows + 7) / 8);
-    const unsigned long long waves = (unsigned long long)WPS * 4;
+    const unsigned long long waves = (unsigned long long)threads / 64u;
     unsigned long long blocks = (unsigned long long)cus * per_cu;
     const unsigned long long need = (tiles + waves - 1) / waves;
     if (blocks > need) blocks = need;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256 * WPS), lds, stream, *a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), lds, stream, *a);
     return hipGetLastError();
 }
 
