@@ -32,7 +32,8 @@ constexpr double SHADOW_BIAS = 1e-13;                 // lib.rs:11
 constexpr float PI_F = 3.14159265358979323846f;       // std::f32::consts::PI
 
 // MODE_WAIT: the lane's top frame awaits a subtree another lane is tracing (task splitting)
-enum : int { MODE_CLOSEST = 0, MODE_SHADOW = 1, MODE_DONE = 2, MODE_WAIT = 3 };
+enum : int { MODE_CLOSEST = 0, MODE_SHADOW = 1, MODE_DONE = 2, MODE_WAIT = 3, MODE_SHADOW_H = 4 };
+// MODE_SHADOW_H: an idle lane tracing one shadow ray for another lane of its wave (shadow fan-out)
 // FR_REFR_TASK / FR_REFR_WAIT carry their pool slot in bits 8+ of Frame::type
 enum : int { FR_REFL = 0, FR_REFR_T = 1, FR_REFR_R = 2, FR_REFL_PEND = 3, FR_REFR_TASK = 4, FR_REFR_WAIT = 5 };
 
@@ -1086,6 +1087,15 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 // refractive pixels (the slowest tiles, which bound a frame's makespan)
 // across the waves of a CU.  Waits only ever point down a tree, so there is
 // no cycle: every awaited subtree is held by a live lane.
+#ifndef RG_SHADOW_FAN
+#define RG_SHADOW_FAN 3   // heavy path: up to this many more lights of a hit traced by idle lanes per iteration
+#endif
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 #ifndef RG_LIGHT_TASKS
 #define RG_LIGHT_TASKS 0   // task splitting on the light path (kernel template parameter TASKS)
 #endif
@@ -1302,6 +1312,9 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     // hit being shaded
     V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0), hd = v3(0, 0, 0);
     int hb = 0, hdepth = 0, li = 0;
+    int nfan = 0;              // shadow fan-out: lights li+1 .. li+nfan of this hit traced by helper lanes
+    uint32_t fan_lanes = 0u;   // ... their lanes, 6 bits each
+    uint32_t fan_bits = 0u;    // ... their occlusion results, bit k
     C3 fin = c3(0, 0, 0), bcol = c3(0, 0, 0), ret = def;
     int sp = 0;
     Closest c;
@@ -1319,6 +1332,21 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     uint32_t tile_iters = 0;
 #endif
     for (;;) {
+        if constexpr (LB == 1 && RG_SHADOW_FAN > 0) {
+            // shadow fan-out, collect: the helpers' occlusion bits (every lane active here)
+            if (__any(nfan > 0)) {
+                fan_bits = 0u;
+#pragma unroll
+                for (int k = 0; k < RG_SHADOW_FAN; ++k) {
+                    const uint32_t b = (uint32_t)__shfl((int)occl, (int)((fan_lanes >> (6 * k)) & 63u), 64);
+                    if (k < nfan) fan_bits |= (b & 1u) << k;
+                }
+            }
+            if (mode == MODE_SHADOW_H) {  // a helper is idle again
+                mode = MODE_DONE;
+                have_result = false;
+            }
+        }
         if (have_result) {
             bool unwind = false;
             bool shade = false;           // run a shade_diffuse step this iteration
@@ -1487,6 +1515,21 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                             C3 lc = cscl(cscl(c3(L.color[0], L.color[1], L.color[2]), power), refl);
                             fin = cadd(fin, cmul(bcol, lc));
                         }
+                    }
+                    if constexpr (LB == 1 && RG_SHADOW_FAN > 0) {
+                        // the lights helper lanes traced, in light order (rendering.rs:141-170)
+                        for (int k = 0; k < nfan; ++k) {
+                            const RgLightDev L = T.lights[li + 1 + k];
+                            V3 ldir;
+                            double ldist;
+                            light_dir_dist(L, hp, ldir, ldist);  // as at setup: same bits
+                            float inten = !((fan_bits >> k) & 1u) ? light_intensity(L, hp) : 0.0f;
+                            float power = fmaxf((float)dot(hn, ldir), 0.0f) * inten;
+                            C3 lc = cscl(cscl(c3(L.color[0], L.color[1], L.color[2]), power), refl);
+                            fin = cadd(fin, cmul(bcol, lc));
+                        }
+                        li += nfan;
+                        nfan = 0;
                     }
                     li += LB;
                 }
@@ -1675,6 +1718,46 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                 continue;
             }
         }
+        if constexpr (LB == 1 && RG_SHADOW_FAN > 0) {
+            // shadow fan-out, assign: a lane about to trace the shadow ray of light li
+            // hands lights li+1.. of the same hit to idle lanes of its wave, so up to
+            // 1 + RG_SHADOW_FAN shadow rays of a hit are traced in one iteration instead
+            // of one per iteration (the slowest pixels' ray trees are chains of such
+            // iterations).  Each helper traces exactly the ray the lane would have.
+            const int want = mode == MODE_SHADOW ? min(a.n_lights - li - 1, RG_SHADOW_FAN) : 0;
+            unsigned long long owners = __ballot(want > 0);
+            if (owners != 0ull) {
+                unsigned long long idle = __ballot(mode == MODE_DONE);
+                while (owners != 0ull && idle != 0ull) {
+                    const int o = __builtin_ctzll(owners);
+                    owners &= owners - 1ull;
+                    const int w = __builtin_amdgcn_readlane(want, o);
+                    const int oli = __builtin_amdgcn_readlane(li, o);
+                    const int ohd = __builtin_amdgcn_readlane(hdepth, o);
+                    const V3 ohp = v3(readlane_d(hp.x, o), readlane_d(hp.y, o), readlane_d(hp.z, o));
+                    const V3 oso = v3(readlane_d(q.o.x, o), readlane_d(q.o.y, o), readlane_d(q.o.z, o));
+                    uint32_t packed = 0u;
+                    int k = 0;
+                    for (; k < w && idle != 0ull; ++k) {
+                        const int hl = __builtin_ctzll(idle);
+                        idle &= idle - 1ull;
+                        packed |= (uint32_t)hl << (6 * k);
+                        if (lane == hl) {
+                            hp = ohp;
+                            q.o = oso;  // hit + n * bias (rendering.rs:148)
+                            hdepth = ohd;
+                            light_dir_dist(T.lights[oli + 1 + k], hp, sb.d[0], sb.ld[0]);
+                            mode = MODE_SHADOW_H;
+                        }
+                    }
+                    if (lane == o) {
+                        nfan = k;
+                        fan_lanes = packed;
+                        n_shadow += (uint32_t)k;
+                    }
+                }
+            }
+        }
         if constexpr (TASKS) {
             // idle lanes take subtrees other lanes of the block published
             const bool idle = mode == MODE_DONE;
@@ -1713,7 +1796,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             __builtin_amdgcn_s_sleep(4);
             continue;
         }
-        const bool querying = mode == MODE_CLOSEST || mode == MODE_SHADOW;  // WAIT lanes only poll
+        const bool querying = mode == MODE_CLOSEST || mode == MODE_SHADOW || mode == MODE_SHADOW_H;  // WAIT lanes only poll
         if (!__any(querying)) {
             __builtin_amdgcn_s_sleep(2);
             have_result = mode == MODE_WAIT;
@@ -1734,9 +1817,10 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                 bool o1 = false;
                 Ray r1;
                 r1.o = q.o;
-                r1.d = mode == MODE_SHADOW ? sb.d[0] : q.d;
-                const bool lane_walk = (mode == MODE_SHADOW ? hdepth : qdepth) >= (int)a.lane_min_depth;
-                trace_query<F32F, BVH>(a, src, r1, mode == MODE_SHADOW, sb.ld[0], c, o1, lane_walk);
+                const bool shadow = mode == MODE_SHADOW || mode == MODE_SHADOW_H;
+                r1.d = shadow ? sb.d[0] : q.d;
+                const bool lane_walk = (shadow ? hdepth : qdepth) >= (int)a.lane_min_depth;
+                trace_query<F32F, BVH>(a, src, r1, shadow, sb.ld[0], c, o1, lane_walk);
                 occl = o1 ? 1u : 0u;
             }
         } else {
