@@ -146,14 +146,16 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     lib = _abi.lib()
     bvh = ds.bvh_info()
 
-    tiling = rd.tiling(rank, world, TILE_ROWS)
+    # --share S (diagnostic, N = 1): render only rank 0's tiles of an S-way split
+    split = args.share if (world == 1 and args.share > 1) else world
+    tiling = rd.tiling(rank, split, TILE_ROWS)
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
-    slot = rd.slot_rows(H, world, TILE_ROWS)  # equal-size gather slots (last ranks zero-padded)
+    slot = rd.slot_rows(H, split, TILE_ROWS)  # equal-size gather slots (last ranks zero-padded)
     out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
     # frames in flight, each on its own render stream and hardware queue (8 per
-    # process, see main): 3 at N = 1, 4 at N > 1, where a rank's share is more
-    # tail-bound (profiles/r01/frames_in_flight_overlap_probe*.json)
-    F = args.frames_in_flight if args.frames_in_flight > 0 else (4 if world > 1 else 3)
+    # process, see main): 3, measured best in this loop for the whole frame and
+    # for a 1/8 share (profiles/r01/bench_frames_in_flight_ab.txt)
+    F = args.frames_in_flight if args.frames_in_flight > 0 else 3
     use_pipe = args.backend == "nccl" or world == 1
     gathered = rd.gather_buffers(out, world) if (world > 1 and rank == 0 and not use_pipe) else None
     frame = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if (rank == 0 and not use_pipe) else None
@@ -337,13 +339,15 @@ def main() -> None:
                     help="rehearsal: every rank renders on GPU 0 (use with --backend gloo)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames in flight, each on its own render stream (N>1: their gathers overlap later renders); "
-                         "0 = 3 at N=1, 4 at N>1")
+                         "0 = 3")
     ap.add_argument("--one-render-stream", action="store_true",
                     help="render every frame on one stream (N>1: only the gathers overlap the renders)")
     ap.add_argument("--roofline-frames", type=int, default=10,
                     help="single-stream launches timed after the timed region for the roofline's kernel time")
     ap.add_argument("--rccl-rehearsal", action="store_true",
                     help="N=1: run the N>1 path anyway (RCCL process group, per-frame gather, re-interleave)")
+    ap.add_argument("--share", type=int, default=1,
+                    help="diagnostic at N=1: time rank 0's share of an S-way split (no gather); value counts its rays")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 checks the gathered frame against a 1-rank render, byte for byte")
     args = ap.parse_args()

@@ -1102,7 +1102,9 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 #ifndef RG_HEAVY_TASKS
 #define RG_HEAVY_TASKS 1   // ... and on the heavy path
 #endif
+#ifndef RG_TASK_SLOTS
 #define RG_TASK_SLOTS 128
+#endif
 struct TaskPool {
     double ray[RG_TASK_SLOTS][6];  // published ray (origin, direction)
     float col[RG_TASK_SLOTS][4];   // the subtree's colour once done
@@ -2063,7 +2065,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     // and with frames in flight the next frame's blocks take the slots of
     // waves that finished (a 4*WPS-wave block would keep the CU until its
     // slowest wave -- one refractive tile -- is done).
-    constexpr int threads = (!BVH && !TASKS) ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS;
+    constexpr int threads = LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS;  // LB > 1: the light path
     static int cus = 0, per_cu = 0;
     static size_t lds_cached = ~(size_t)0;
     auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH, TASKS>;
