@@ -10,7 +10,10 @@ then re-interleaved into image order on rank 0.
 
 Workload (BASELINE.json configs[1]): examples/test1.yml at 3840x2160,
 recursion depth 5, 1 GPU.  `--workload synth1024` selects the north_star's
-1024-sphere 3840x2160 depth-5 scene instead.
+1024-sphere 3840x2160 depth-5 scene instead.  Two extra line items report the
+north_star scene at 3840x2160 and at 7680x4320 (BASELINE configs[3]) on the
+same N GPUs.  Frames are kept in flight (4, each on its own render stream):
+the timed region holds `--steps` complete frames.
 
 Prints ONE JSON line on rank 0 (the driver's contract) with `roofline`
 (FP64-VALU bound, from HIP events on the render stream), `roofline_hbm`
@@ -38,7 +41,7 @@ OPS_PER_BODY = {"sphere": 16, "plane": 14, "disk": 20, "aabb": 18}
 TILE_ROWS = 16
 
 
-def load_workload(name: str):
+def load_workload(name: str, W: int = 3840, H: int = 2160):
     from raingun_amd.scene import AABB, Disk, Plane, Sphere, load_scene
     from raingun_amd.synth import scene_md5, synthetic_yaml
 
@@ -46,19 +49,21 @@ def load_workload(name: str):
     if name == "test1":
         scene = load_scene(golden / "examples" / "test1.yml", texture_root=golden)
         scene.max_recursion_depth = 5
-        label = "examples/test1.yml 3840x2160 depth 5 (BASELINE configs[1])"
+        label = f"examples/test1.yml {W}x{H} depth 5 (BASELINE configs[1])"
         src = ("reference example scene examples/test1.yml; textures decoded by the native host layer "
                "(libraingun_host.so, jpeg-decoder 0.1.11 rounding)")
     elif name == "test3":
         scene = load_scene(golden / "examples" / "test3.yml", texture_root=golden)
-        label = "examples/test3.yml 3840x2160 depth 10 (BASELINE configs[2])"
+        label = f"examples/test3.yml {W}x{H} depth 10 (BASELINE configs[2])"
         src = ("reference example scene examples/test3.yml; textures decoded by the native host layer "
                "(libraingun_host.so, jpeg-decoder 0.1.11 rounding)")
     elif name.startswith("synth"):
         n = int(name[5:] or 1024)
         text = synthetic_yaml(n, 2, 5)
         scene = load_scene(text)
-        label = f"synthetic {n} spheres + 2 planes 3840x2160 depth 5 (seed 0x5EED, md5 {scene_md5(text)})"
+        label = f"synthetic {n} spheres + 2 planes {W}x{H} depth 5 (seed 0x5EED, md5 {scene_md5(text)})"
+        if (W, H) == (7680, 4320):
+            label += " (BASELINE configs[3])"
         src = "synthetic seeded scene (raingun_amd/synth.py)"
     else:
         raise SystemExit(f"unknown workload {name}")
@@ -129,7 +134,7 @@ def load_traffic(workload: str, n_gpus: int):
         return None
 
 
-def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cpu: bool):
+def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cpu: bool, size=None):
     """Time `args.steps` frames of `workload` on this rank (after `args.warmup`),
     frame sharded over `world` ranks and gathered to rank 0.  Returns the
     rank-0 result dict (None on other ranks)."""
@@ -140,8 +145,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     from raingun_amd import distributed as rd
     from raingun_amd.scene import DeviceScene
 
-    scene, label, src, body_counts, ops_per_ray = load_workload(workload)
-    W, H = args.width, args.height
+    W, H = size or (args.width, args.height)
+    scene, label, src, body_counts, ops_per_ray = load_workload(workload, W, H)
     ds = DeviceScene(scene, device=local_rank)  # scene + textures uploaded once, resident in HBM
     lib = _abi.lib()
     bvh = ds.bvh_info()
@@ -333,7 +338,7 @@ def main() -> None:
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-north-star", action="store_true",
-                    help="skip the extra north_star line item (1024 spheres, 3840x2160, depth 5)")
+                    help="skip the extra north_star line items (1024 spheres, depth 5, 3840x2160 and 7680x4320)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo: rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank renders on GPU 0 (use with --backend gloo)")
@@ -386,9 +391,13 @@ def main() -> None:
     cpu = (not args.no_cpu_baseline) and world == 1
 
     main_res = measure(args.workload, args, world, rank, local_rank, dev, cpu)
-    ns_res = None
+    ns_res = ns8k_res = None
     if not args.no_north_star and args.workload != "synth1024":
         ns_res = measure("synth1024", args, world, rank, local_rank, dev, cpu)
+    if not args.no_north_star:
+        # BASELINE configs[3]: the north-star scene at 7680x4320, row-tiled over the N GPUs
+        # (the CPU rate per ray is the 3840x2160 line's: same scene, same rays per pixel)
+        ns8k_res = measure("synth1024", args, world, rank, local_rank, dev, False, size=(7680, 4320))
 
     if rank == 0:
         line = {
@@ -407,6 +416,8 @@ def main() -> None:
         line.update({k: v for k, v in main_res.items() if k not in ("value", "ms_per_step")})
         if ns_res is not None:
             line["north_star_1024_spheres"] = ns_res
+        if ns8k_res is not None:
+            line["north_star_1024_spheres_8k"] = ns8k_res
         print(json.dumps(line), file=json_out, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
