@@ -1,7 +1,7 @@
 // rg_kernels.hip — the render megakernel for gfx950 (MI355X).
 //
-// One lane = one pixel.  A wave covers an 8x8 pixel quad (ray coherence), a
-// 256-thread workgroup a 16x16 tile.  The reference's recursion
+// One lane = one pixel.  A wave renders 8x8 pixel tiles (ray coherence) taken
+// from a sharded atomic queue.  The reference's recursion
 //   render_pixel -> get_color -> {shade_diffuse | cast_ray -> get_color ...}
 // (raingun-lib/src/rendering.rs:71-172) becomes a per-lane state machine:
 // every loop iteration each live lane owns exactly ONE query ray (closest-hit
@@ -1087,6 +1087,18 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 // refractive pixels (the slowest tiles, which bound a frame's makespan)
 // across the waves of a CU.  Waits only ever point down a tree, so there is
 // no cycle: every awaited subtree is held by a live lane.
+// Light path, non-persistent waves: a wave renders at most this many 8x8 tiles
+// and exits, and the grid holds one wave per that many tiles, so the hardware
+// dispatcher hands out CU slots wave by wave -- across the kernels of frames in
+// flight too -- instead of 3072 persistent waves pinning their slots until the
+// frame's queue is empty.  0 = persistent.  16 measured best for the whole 4K
+// frame and for 1/2 .. 1/8 shares (profiles/r01/variants_light_tiles_per_wave.txt).
+#ifndef RG_LIGHT_TILES_PER_WAVE
+#define RG_LIGHT_TILES_PER_WAVE 16
+#endif
+#ifndef RG_HEAVY_TILES_PER_WAVE
+#define RG_HEAVY_TILES_PER_WAVE 0  // heavy path: 0 = persistent blocks (one per CU)
+#endif
 #ifndef RG_SHADOW_FAN
 #define RG_SHADOW_FAN 3   // heavy path: up to this many more lights of a hit traced by idle lanes per iteration
 #endif
@@ -1217,12 +1229,13 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
     for (uint32_t k = threadIdx.x; k < bytes / 16u; k += blockDim.x) d[k] = g[k];
 }
 
-// Persistent render kernel: ONE block of 256*WPS threads per CU (WPS waves
-// per SIMD).  The block stages the scene into LDS once (LSPH: sphere tables;
-// LCOLD: bodies, materials, lights, texture descriptors), then every wave
-// repeatedly takes the next 8x8 pixel tile from an atomic queue
-// (counters[16..], sharded) and runs the per-lane state machine until its 64 lanes have
-// written their pixels.
+// Render kernel.  Heavy path: ONE persistent block of 256*WPS threads per CU
+// (WPS waves per SIMD).  Light path: one-wave blocks, each rendering at most
+// RG_LIGHT_TILES_PER_WAVE tiles (launcher: launch_one).  A block stages the
+// scene into LDS (LSPH: sphere tables; LCOLD: bodies, materials, lights,
+// texture descriptors), then every wave repeatedly takes the next 8x8 pixel
+// tile from an atomic queue (counters[16..], sharded) and runs the per-lane
+// state machine until its 64 lanes have written their pixels.
 template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
 __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     static_assert(!BVH || 4 * WPS <= RG_BVH_MAX_WAVES, "one BVH stack per wave");
@@ -1327,6 +1340,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     uint32_t pixel = 0;        // image pixel index (error reports) of the lane's pixel or task
     int task = -1;             // pool slot whose subtree this lane computes (-1: its own pixel)
     bool tiles_left = true;    // the tile queue has not been found empty
+    [[maybe_unused]] uint32_t tiles_taken = 0;
     [[maybe_unused]] bool counted = false;  // this wave is counted in rg_pool.busy
 #ifdef RG_TILE_TIMES
     uint32_t cur_tile = 0xFFFFFFFFu;  // diagnostic: per-tile time into rgb[tile] (us), wave iterations
@@ -1682,6 +1696,12 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             if (tile == 0xFFFFFFFFu) {
                 tiles_left = false;
             } else {
+                constexpr uint32_t kmax = LB > 1 ? RG_LIGHT_TILES_PER_WAVE : RG_HEAVY_TILES_PER_WAVE;
+                if constexpr (kmax > 0) {
+                    // non-persistent: a wave renders at most kmax tiles, so the grid
+                    // drains through the hardware dispatcher wave (block) by wave
+                    if (++tiles_taken >= kmax) tiles_left = false;
+                }
                 if (a.tile_perm) tile = a.tile_perm[tile];  // scheduling order only; every tile is rendered once
                 const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
 #ifdef RG_TILE_TIMES
@@ -2088,6 +2108,9 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     unsigned long long blocks = (unsigned long long)cus * per_cu;
     const unsigned long long need = (tiles + waves - 1) / waves;
     if (blocks > need) blocks = need;
+    constexpr unsigned long long kmax = LB > 1 ? RG_LIGHT_TILES_PER_WAVE : RG_HEAVY_TILES_PER_WAVE;
+    if constexpr (kmax > 0)  // non-persistent: one wave per kmax tiles
+        blocks = (tiles + waves * kmax - 1) / (waves * kmax);
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), lds, stream, *a);
     return hipGetLastError();
