@@ -189,12 +189,18 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     # at N > 1 gathered and assembled on rank 0) when the timed region ends.
     # The gloo rehearsal gathers through host memory one frame at a time.
     pipe = None
-    if use_pipe:
+    gather = world > 1 or args.rccl_rehearsal
+    native = use_pipe and gather and args.backend == "nccl" and not args.python_pipeline
+    if native:  # the per-frame loop in C++ (include/raingun_frames.h): render, ncclGather, re-interleave
+        pipe = rd.NativeFramePipeline(ds.handle, W, H, rank, world, TILE_ROWS, depth=F, device=dev)
+    elif use_pipe:
         pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TILE_ROWS, device=dev, depth=F,
-                                streams=F > 1 and not args.one_render_stream, gather=world > 1 or args.rccl_rehearsal)
+                                streams=F > 1 and not args.one_render_stream, gather=gather)
 
     def step():
-        if pipe is not None:
+        if native:
+            pipe.step()
+        elif pipe is not None:
             pipe.step(lambda part: render(buf=part))
         else:
             rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
@@ -252,7 +258,11 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     elapsed = float(tt[0])
     verified = None
     if getattr(args, "verify", False):
-        if pipe is not None:
+        if native:
+            step()
+            finish()
+            final = pipe.read_frame() if rank == 0 else None
+        elif pipe is not None:
             step()
             finish()
             final = pipe.frame if rank == 0 else None
@@ -261,9 +271,14 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         if rank == 0:
             torch.cuda.synchronize(dev)
             ref = ds.render_image(W, H)
-            verified = bool((final.cpu().numpy() == ref).all())
+            import numpy as np
+
+            got = final if isinstance(final, np.ndarray) else final.cpu().numpy()
+            verified = bool((got == ref).all())
             if not verified:
                 raise SystemExit(f"--verify: the {world}-rank frame differs from the 1-rank render")
+    if native:
+        pipe.close()
     ds.close()
     if rank != 0:
         return None
@@ -272,7 +287,9 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         parallelism = f"row-tiles x{world} (round-robin 16-row tiles, one RCCL gather per frame to rank 0"
     else:
         parallelism = "one GPU (whole frame"
-    if pipe is not None and pipe.streams:
+    if native:
+        parallelism += f", {F} frames in flight on {F} render streams; per-frame loop in C++, raingun_frames.h)"
+    elif pipe is not None and pipe.streams:
         parallelism += f", {F} frames in flight on {F} render streams)"
     else:
         parallelism += ", frames rendered one after another on one stream)"
@@ -351,6 +368,8 @@ def main() -> None:
                     help="single-stream launches timed after the timed region for the roofline's kernel time")
     ap.add_argument("--rccl-rehearsal", action="store_true",
                     help="N=1: run the N>1 path anyway (RCCL process group, per-frame gather, re-interleave)")
+    ap.add_argument("--python-pipeline", action="store_true",
+                    help="N>1: run the per-frame loop in Python (raingun_amd.distributed.FramePipeline)")
     ap.add_argument("--share", type=int, default=1,
                     help="diagnostic at N=1: time rank 0's share of an S-way split (no gather); value counts its rays")
     ap.add_argument("--verify", action="store_true",

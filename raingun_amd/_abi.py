@@ -132,6 +132,9 @@ EXPORTED_SYMBOLS = (
 # include/raingun_debug.h
 DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
                  "rg_debug_set_tile_order", "rg_debug_set_lane_depth")
+# include/raingun_frames.h
+FRAMES_SYMBOLS = ("rg_frames_create", "rg_frames_destroy", "rg_frames_step", "rg_frames_flush", "rg_frames_image",
+                  "rg_frames_read_image")
 PATH_AUTO, PATH_LIGHT, PATH_HEAVY = -1, 0, 1
 
 
@@ -184,6 +187,19 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_set_lane_depth.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_counters.restype = C.c_int32
     lib.rg_debug_counters.argtypes = [C.c_void_p, P(C.c_uint64)]
+    lib.rg_frames_create.restype = C.c_int32
+    lib.rg_frames_create.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_int32,
+                                     C.c_int32, C.c_void_p, C.c_void_p, P(C.c_void_p)]
+    lib.rg_frames_destroy.restype = None
+    lib.rg_frames_destroy.argtypes = [C.c_void_p]
+    lib.rg_frames_step.restype = C.c_int32
+    lib.rg_frames_step.argtypes = [C.c_void_p]
+    lib.rg_frames_flush.restype = C.c_int32
+    lib.rg_frames_flush.argtypes = [C.c_void_p]
+    lib.rg_frames_image.restype = C.c_void_p
+    lib.rg_frames_image.argtypes = [C.c_void_p]
+    lib.rg_frames_read_image.restype = C.c_int32
+    lib.rg_frames_read_image.argtypes = [C.c_void_p, C.c_void_p]
     lib.rg_trace.restype = C.c_int32
     lib.rg_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
 

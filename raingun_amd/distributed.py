@@ -258,3 +258,79 @@ class FramePipeline:
         if self.streams is not None:  # the renders (one rank: nothing else follows them)
             for s in self.streams:
                 torch.cuda.current_stream().wait_stream(s)
+
+
+def rccl_gather_fn() -> int:
+    """Address of ncclGather in the RCCL PyTorch loaded (the library behind its
+    "nccl" process group), for rg_frames_create."""
+    import ctypes as C
+    import os
+
+    import torch
+
+    rccl = C.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))  # already loaded: same instance
+    return C.cast(rccl.ncclGather, C.c_void_p).value
+
+
+def rccl_comm_ptr(group=None, device=None) -> int:
+    """The ncclComm_t of a torch.distributed "nccl" process group (created by a
+    first collective if the group initialises lazily)."""
+    import torch
+    import torch.distributed as dist
+
+    pg = group if group is not None else dist.distributed_c10d._get_default_group()
+    dist.all_reduce(torch.zeros(1, device=device), group=pg)
+    return pg._get_backend(torch.device("cuda", torch.cuda.current_device()))._comm_ptr()
+
+
+class NativeFramePipeline:
+    """FramePipeline's N > 1 loop in C++ (include/raingun_frames.h): frame k
+    renders on render stream k % depth, ONE ncclGather per frame runs on a
+    communication stream in frame order, rank 0 re-interleaves on a side stream
+    -- a handful of HIP/RCCL calls per frame instead of ~70 us of Python on
+    rank 0, which would otherwise bound a small share (1/8 of a 4K test1 frame
+    renders in ~55 us).  Uses the communicator of the torch.distributed "nccl"
+    group and the RCCL library torch loaded."""
+
+    def __init__(self, scene_handle, width: int, height: int, rank: int, world: int, tile_rows: int = TILE_ROWS,
+                 depth: int = 4, group=None, device=None):
+        import ctypes as C
+
+        from . import _abi
+
+        self.W, self.H, self.rank = width, height, rank
+        self._lib = _abi.lib()
+        h = C.c_void_p()
+        st = self._lib.rg_frames_create(scene_handle, width, height, tile_rows, rank, world, depth,
+                                        C.c_void_p(rccl_comm_ptr(group, device)), C.c_void_p(rccl_gather_fn()),
+                                        C.byref(h))
+        _abi.check(st, "rg_frames_create")
+        self._h = h
+
+    def step(self, render=None):
+        from . import _abi
+
+        _abi.check(self._lib.rg_frames_step(self._h), "rg_frames_step")
+
+    def flush(self):
+        from . import _abi
+
+        _abi.check(self._lib.rg_frames_flush(self._h), "rg_frames_flush")
+
+    def read_frame(self):
+        """Rank 0: the latest assembled frame as a (H, W, 4) uint8 numpy array."""
+        import numpy as np
+
+        from . import _abi
+
+        out = np.empty((self.H, self.W, 4), dtype=np.uint8)
+        _abi.check(self._lib.rg_frames_read_image(self._h, out.ctypes.data), "rg_frames_read_image")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.rg_frames_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()

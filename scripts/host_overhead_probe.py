@@ -62,6 +62,10 @@ for f, gather in ((1, False), (4, False), (4, True)):
     timed(f"pipeline_F{f}{'_gather' if gather else ''}",
           lambda: pipe.step(lambda part: launch(part, torch.cuda.current_stream())))
     pipe.flush()
+native = rd.NativeFramePipeline(ds.handle, W, H, 0, 1, T, depth=4, device=dev)
+timed("native_pipeline_F4_gather", native.step)
+native.flush()
+native.close()
 recv = [torch.empty_like(buf)]
 timed("dist.gather_alone", lambda: dist.gather(buf, recv, dst=0, async_op=True))
 print(json.dumps(out, indent=1))

@@ -28,13 +28,15 @@ def libpath():
 def test_header_matches_binding_table():
     assert declared_functions() == sorted(_abi.EXPORTED_SYMBOLS)
     assert declared_functions(INCLUDE / "raingun_debug.h") == sorted(_abi.DEBUG_SYMBOLS)
+    assert declared_functions(INCLUDE / "raingun_frames.h") == sorted(_abi.FRAMES_SYMBOLS)
 
 
 def test_library_exports_every_symbol(libpath):
     out = subprocess.run(["nm", "-D", "--defined-only", str(libpath)], capture_output=True, text=True,
                          check=True).stdout
     exported = {l.split()[-1] for l in out.splitlines() if l.strip()}
-    declared = declared_functions() + declared_functions(INCLUDE / "raingun_debug.h")
+    declared = (declared_functions() + declared_functions(INCLUDE / "raingun_debug.h")
+                + declared_functions(INCLUDE / "raingun_frames.h"))
     missing = [s for s in declared if s not in exported]
     assert not missing, missing
 
@@ -57,6 +59,11 @@ def test_invalid_arguments_fail_loudly(libpath):
     assert lib.rg_scene_create(None, 0, None) == _abi.RG_ERR_INVALID_ARGUMENT
     assert lib.rg_render_image(None, 8, 8, None, None) == _abi.RG_ERR_INVALID_ARGUMENT
     assert lib.rg_trace(None, None, 1, None, None) == _abi.RG_ERR_INVALID_ARGUMENT
+    out = C.c_void_p(7)
+    assert lib.rg_frames_create(None, 8, 8, 16, 0, 1, 2, None, None, C.byref(out)) == _abi.RG_ERR_INVALID_ARGUMENT
+    assert out.value is None
+    assert lib.rg_frames_step(None) == _abi.RG_ERR_INVALID_ARGUMENT
+    assert lib.rg_frames_image(None) is None
 
 
 def test_struct_sizes_match_header():
