@@ -148,6 +148,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     W, H = size or (args.width, args.height)
     scene, label, src, body_counts, ops_per_ray = load_workload(workload, W, H)
     ds = DeviceScene(scene, device=local_rank)  # scene + textures uploaded once, resident in HBM
+    if args.tile_order >= 0:
+        ds.set_tile_order(args.tile_order)
     lib = _abi.lib()
     bvh = ds.bvh_info()
 
@@ -370,6 +372,8 @@ def main() -> None:
                     help="N=1: run the N>1 path anyway (RCCL process group, per-frame gather, re-interleave)")
     ap.add_argument("--python-pipeline", action="store_true",
                     help="N>1: run the per-frame loop in Python (raingun_amd.distributed.FramePipeline)")
+    ap.add_argument("--tile-order", type=int, default=-1,
+                    help="diagnostic: 1 = probe-ordered tiles, 0 = raster order, -1 = library default")
     ap.add_argument("--share", type=int, default=1,
                     help="diagnostic at N=1: time rank 0's share of an S-way split (no gather); value counts its rays")
     ap.add_argument("--verify", action="store_true",
