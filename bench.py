@@ -155,9 +155,10 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
 
     # --share S (diagnostic, N = 1): render only rank 0's tiles of an S-way split
     split = args.share if (world == 1 and args.share > 1) else world
-    tiling = rd.tiling(rank, split, TILE_ROWS)
+    TR = args.tile_rows  # rows per interleaved row tile (rank t % N renders tile t)
+    tiling = rd.tiling(args.share_rank if split != world else rank, split, TR)
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
-    slot = rd.slot_rows(H, split, TILE_ROWS)  # equal-size gather slots (last ranks zero-padded)
+    slot = rd.slot_rows(H, split, TR)  # equal-size gather slots (last ranks zero-padded)
     out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
     # frames in flight, each on its own render stream and hardware queue (8 per
     # process, see main): 4, measured best in this loop for the whole frame and
@@ -194,9 +195,9 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     gather = world > 1 or args.rccl_rehearsal
     native = use_pipe and gather and args.backend == "nccl" and not args.python_pipeline
     if native:  # the per-frame loop in C++ (include/raingun_frames.h): render, ncclGather, re-interleave
-        pipe = rd.NativeFramePipeline(ds.handle, W, H, rank, world, TILE_ROWS, depth=F, device=dev)
+        pipe = rd.NativeFramePipeline(ds.handle, W, H, rank, world, TR, depth=F, device=dev)
     elif use_pipe:
-        pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TILE_ROWS, device=dev, depth=F,
+        pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TR, device=dev, depth=F,
                                 streams=F > 1 and not args.one_render_stream, gather=gather)
 
     def step():
@@ -205,7 +206,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         elif pipe is not None:
             pipe.step(lambda part: render(buf=part))
         else:
-            rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
+            rd.render_frame(render_tiles, H, rank, world, TR, out=frame, gather_bufs=gathered)
 
     def finish():
         if pipe is not None:
@@ -269,7 +270,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
             finish()
             final = pipe.frame if rank == 0 else None
         else:
-            final = rd.render_frame(render_tiles, H, rank, world, TILE_ROWS, out=frame, gather_bufs=gathered)
+            final = rd.render_frame(render_tiles, H, rank, world, TR, out=frame, gather_bufs=gathered)
         if rank == 0:
             torch.cuda.synchronize(dev)
             ref = ds.render_image(W, H)
@@ -286,7 +287,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         return None
 
     if world > 1:
-        parallelism = f"row-tiles x{world} (round-robin 16-row tiles, one RCCL gather per frame to rank 0"
+        parallelism = f"row-tiles x{world} (round-robin {TR}-row tiles, one RCCL gather per frame to rank 0"
     else:
         parallelism = "one GPU (whole frame"
     if native:
@@ -309,7 +310,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         "kernel_ms": round(kernel_ms, 4),
         "data": src,
         "config": {"workload": label, "width": W, "height": H, "max_recursion_depth": scene.max_recursion_depth,
-                   "bodies": body_counts, "lights": len(scene.lights), "tile_rows": TILE_ROWS,
+                   "bodies": body_counts, "lights": len(scene.lights), "tile_rows": TR,
                    "parallelism": parallelism},
         "rays_per_frame": {"primary": rays[0], "shadow": rays[1], "secondary": rays[2], "total": rays_per_frame},
         "roofline": {
@@ -372,6 +373,10 @@ def main() -> None:
                     help="N=1: run the N>1 path anyway (RCCL process group, per-frame gather, re-interleave)")
     ap.add_argument("--python-pipeline", action="store_true",
                     help="N>1: run the per-frame loop in Python (raingun_amd.distributed.FramePipeline)")
+    ap.add_argument("--tile-rows", type=int, default=8,
+                    help="rows per interleaved row tile of the N-way split (8: the slowest of 8 shares is 2-4 %% "
+                         "faster than with 16, profiles/r01/bench_rank_shares.txt)")
+    ap.add_argument("--share-rank", type=int, default=0, help="diagnostic: which rank's share --share times")
     ap.add_argument("--tile-order", type=int, default=-1,
                     help="diagnostic: 1 = probe-ordered tiles, 0 = raster order, -1 = library default")
     ap.add_argument("--share", type=int, default=1,
