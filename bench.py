@@ -195,8 +195,12 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     gather = world > 1 or args.rccl_rehearsal
     native = use_pipe and gather and args.backend == "nccl" and not args.python_pipeline
     if native:  # the per-frame loop in C++ (include/raingun_frames.h): render, ncclGather, re-interleave
-        pipe = rd.NativeFramePipeline(ds.handle, W, H, rank, world, TR, depth=F, device=dev)
-    elif use_pipe:
+        try:
+            pipe = rd.NativeFramePipeline(ds.handle, W, H, rank, world, TR, depth=F, device=dev)
+        except Exception as e:  # e.g. no communicator pointer from this torch build: same loop in Python
+            print(f"[bench] native frame pipeline unavailable ({e}); using the Python loop", file=sys.stderr)
+            native = False
+    if not native and use_pipe:
         pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TR, device=dev, depth=F,
                                 streams=F > 1 and not args.one_render_stream, gather=gather)
 
