@@ -149,10 +149,11 @@ rg_status rg_frames_step(rg_frames *f) {
     if (st != RG_OK) return st;
     if (!ok(hipEventRecord(f->rendered[b], rs)) || !ok(hipStreamWaitEvent(f->comm_stream, f->rendered[b], 0)))
         return RG_ERR_DEVICE;
-    // ncclUint8 = 1 (rccl.h); recvbuff may be NULL off the root
-    if (f->gather(f->parts[b], f->rank == 0 ? f->gathered[b] : nullptr, f->part_bytes, 1, 0, f->comm,
-                  f->comm_stream) != 0)
-        return RG_ERR_DEVICE;
+    // ncclUint8 = 1 (rccl.h); recvbuff may be NULL off the root.  ncclSuccess = 0;
+    // a non-blocking communicator may answer ncclInProgress = 7 with the operation enqueued
+    const int gr = f->gather(f->parts[b], f->rank == 0 ? f->gathered[b] : nullptr, f->part_bytes, 1, 0, f->comm,
+                             f->comm_stream);
+    if (gr != 0 && gr != 7) return RG_ERR_DEVICE;
     if (!ok(hipEventRecord(f->sent[b], f->comm_stream))) return RG_ERR_DEVICE;
     if (f->rank == 0) {
         if (!ok(hipStreamWaitEvent(f->side, f->sent[b], 0))) return RG_ERR_DEVICE;
