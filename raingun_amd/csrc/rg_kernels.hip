@@ -1112,7 +1112,15 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 #define RG_LIGHT_TASKS 0   // task splitting on the light path (kernel template parameter TASKS)
 #endif
 #ifndef RG_HEAVY_TASKS
-#define RG_HEAVY_TASKS 1   // ... and on the heavy path
+#define RG_HEAVY_TASKS 1   // ... and on the heavy path, for launches of fewer than RG_HEAVY_TASK_TILES tiles
+#endif
+#ifndef RG_HEAVY_TASK_TILES
+// Task splitting shortens the slowest pixels' ray trees, which bound a small
+// launch; on a large one (and with frames in flight, whose next frame fills
+// the tail) its bookkeeping costs more than it saves: with 4 frames in flight
+// synth1024 4K 3.10 -> 2.88 ms and 8K 11.18 -> 9.94 ms without it, but a 1/8
+// share (16k tiles) 0.538 -> 0.561 ms (profiles/r01/variants_heavy_tasks.txt)
+#define RG_HEAVY_TASK_TILES 24576
 #endif
 #ifndef RG_TASK_SLOTS
 #define RG_TASK_SLOTS 128
@@ -2148,8 +2156,13 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
     // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
     const bool heavy = rg_heavy_path(*a);
     if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream);
-    if (a->n_nodes > 0) return launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, RG_HEAVY_TASKS>(a, stream);
-    return launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, RG_HEAVY_TASKS>(a, stream);
+    const unsigned long long tiles = (unsigned long long)((a->width + 7) / 8) * ((a->out_rows + 7) / 8);
+    const bool tasks = RG_HEAVY_TASKS && tiles < RG_HEAVY_TASK_TILES;
+    if (a->n_nodes > 0)
+        return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, true>(a, stream)
+                     : launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, false>(a, stream);
+    return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, true>(a, stream)
+                 : launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, false>(a, stream);
 }
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {
