@@ -4,9 +4,10 @@
 One step = one frame of the workload rendered by the HIP megakernel, scene and
 textures already resident in HBM, framebuffer left in HBM (rank 0 holds the
 assembled frame).  At N>1 (torchrun, one rank per GPU) the frame is cut into
-16-row tiles dealt round-robin to the ranks and the tiles are gathered to rank
-0 with one RCCL gather (torch.distributed backend "nccl" = RCCL over xGMI),
-then re-interleaved into image order on rank 0.
+8-row tiles dealt round-robin to the ranks and the tiles are gathered to rank
+0 with one RCCL gather per frame (ncclGather on the communicator of the
+torch.distributed "nccl" group, i.e. RCCL over xGMI), then re-interleaved into
+image order on rank 0 -- the per-frame loop runs in C++ (include/raingun_frames.h).
 
 Workload (BASELINE.json configs[1]): examples/test1.yml at 3840x2160,
 recursion depth 5, 1 GPU.  `--workload synth1024` selects the north_star's
