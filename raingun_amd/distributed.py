@@ -333,4 +333,7 @@ class NativeFramePipeline:
             self._h = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown: the runtime may already be gone
+            pass
