@@ -161,10 +161,10 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
     slot = rd.slot_rows(H, split, TR)  # equal-size gather slots (last ranks zero-padded)
     out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
-    # frames in flight, each on its own render stream and hardware queue (8 per
-    # process, see main): 4, measured best in this loop for the whole frame and
-    # for a 1/8 share (profiles/r01/bench_frames_in_flight_ab.txt)
-    F = args.frames_in_flight if args.frames_in_flight > 0 else 4
+    # frames in flight, each on its own render stream and hardware queue (12 per
+    # process, see main): 6 -- the whole frame is flat from 4 up, a 1/8 test1
+    # share gains 12 % from 4 to 6 (profiles/r01/bench_frames_in_flight_ab.txt)
+    F = args.frames_in_flight if args.frames_in_flight > 0 else 6
     use_pipe = args.backend == "nccl" or world == 1
     gathered = rd.gather_buffers(out, world) if (world > 1 and rank == 0 and not use_pipe) else None
     frame = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if (rank == 0 and not use_pipe) else None
@@ -369,7 +369,7 @@ def main() -> None:
                     help="rehearsal: every rank renders on GPU 0 (use with --backend gloo)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames in flight, each on its own render stream (N>1: their gathers overlap later renders); "
-                         "0 = 4")
+                         "0 = 6")
     ap.add_argument("--one-render-stream", action="store_true",
                     help="render every frame on one stream (N>1: only the gathers overlap the renders)")
     ap.add_argument("--roofline-frames", type=int, default=10,
@@ -395,8 +395,9 @@ def main() -> None:
     # frames in flight need a hardware queue per render stream next to RCCL's
     # stream and rank 0's re-interleave stream (HIP's default is 4 per process)
     # (the GPU box exports HIP's default, 4, so raise it rather than default it)
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    # 6 render streams + RCCL's + the communication and side streams + the null stream
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 12:
+        os.environ["GPU_MAX_HW_QUEUES"] = "12"
     sys.stdout.flush()
     os.dup2(2, 1)
 
