@@ -66,6 +66,14 @@ native = rd.NativeFramePipeline(ds.handle, W, H, 0, 1, T, depth=4, device=dev)
 timed("native_pipeline_F4_gather", native.step)
 native.flush()
 native.close()
+# the same loop with a no-op in place of ncclGather: the library's own host cost
+NOOP = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_void_p, C.c_void_p)(
+    lambda *a: 0)
+h = C.c_void_p()
+_abi.check(lib.rg_frames_create(ds.handle, W, H, T, 0, 1, 4, C.c_void_p(1), C.cast(NOOP, C.c_void_p), C.byref(h)))
+timed("native_pipeline_F4_noop_gather", lambda: _abi.check(lib.rg_frames_step(h)))
+lib.rg_frames_flush(h)
+lib.rg_frames_destroy(h)
 recv = [torch.empty_like(buf)]
 timed("dist.gather_alone", lambda: dist.gather(buf, recv, dst=0, async_op=True))
 print(json.dumps(out, indent=1))
