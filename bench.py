@@ -292,7 +292,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         return None
 
     if world > 1:
-        parallelism = f"row-tiles x{world} (round-robin {TR}-row tiles, one RCCL gather per frame to rank 0"
+        via = "RCCL" if args.backend == "nccl" else f"{args.backend} (rehearsal, through host memory)"
+        parallelism = f"row-tiles x{world} (round-robin {TR}-row tiles, one {via} gather per frame to rank 0"
     else:
         parallelism = "one GPU (whole frame"
     if native:
