@@ -30,4 +30,8 @@ struct RgBvhBuild {
 bool rg_build_bvh(const double *spheres, int n, RgBvhBuild &out);
 
 // Largest sphere count per leaf.
-constexpr int RG_BVH_LEAF_MAX = 4;
+#ifndef RG_BVH_LEAF_SPHERES
+#define RG_BVH_LEAF_SPHERES 4  // at most 8: a leaf link keeps (count - 1) in 3 bits
+#endif
+constexpr int RG_BVH_LEAF_MAX = RG_BVH_LEAF_SPHERES;
+static_assert(RG_BVH_LEAF_MAX >= 1 && RG_BVH_LEAF_MAX <= 8, "leaf link format");
