@@ -124,13 +124,14 @@ def cpu_baseline(scene, width, height, budget_s: float = 12.0):
     }
 
 
-def load_traffic(workload: str, n_gpus: int):
+def load_traffic(workload: str, n_gpus: int, key: str = "hbm_bytes_per_launch"):
+    """A PMC figure for this workload's kernel (scripts/pmc.sh -> profiles/traffic.json)."""
     f = REPO / "profiles" / "traffic.json"
     if n_gpus != 1 or not f.exists():
         return None
     try:
         d = json.loads(f.read_text())
-        return d.get(workload, {}).get("hbm_bytes_per_launch")
+        return d.get(workload, {}).get(key)
     except Exception:
         return None
 
@@ -326,6 +327,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
             "unit": "TFLOP/s",
             "frac": round(achieved_t / FP64_PEAK_TOPS, 5),
             "traffic": traffic,
+            "valu_busy_pmc": load_traffic(workload, world, "valu_busy") if (W, H) == (3840, 2160) else None,
             "basis": f"reference-equivalent work: {ops_per_ray} FP64 ops per ray (16/sphere, 14/plane, 20/disk, "
                      f"18/aabb; SURVEY.md 8d) x {my_rays} rays per launch / mean rg_render_kernel time (HIP events "
                      f"around {max(1, args.roofline_frames)} single-stream launches after the timed region)" + (

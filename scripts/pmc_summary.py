@@ -51,12 +51,20 @@ def main():
             "fetch_bytes_raw": a.get("FETCH_SIZE", 0) * 1024,
             "write_bytes": a.get("WRITE_SIZE", 0) * 1024,
             "hbm_bytes_per_launch": (a.get("FETCH_SIZE", 0) * 2 + a.get("WRITE_SIZE", 0)) * 1024,
+            # VALU pipe utilisation: 4 cycles per wave64 VALU instruction on a 16-lane SIMD, over
+            # 1,024 SIMDs x kernel cycles (SQ_BUSY_CYCLES is summed over the 32 shader engines)
+            "valu_busy": (a["SQ_INSTS_VALU"] * 4.0 / (1024.0 * a["SQ_BUSY_CYCLES"] / 32.0)
+                          if a.get("SQ_INSTS_VALU") and a.get("SQ_BUSY_CYCLES") else None),
+            "lds_active": (a["SQ_LDS_IDX_ACTIVE"] / 256.0 / (a["SQ_BUSY_CYCLES"] / 32.0)
+                           if a.get("SQ_LDS_IDX_ACTIVE") and a.get("SQ_BUSY_CYCLES") else None),
         }
         out = REPO / "profiles" / rnd / "pmc"
         out.mkdir(parents=True, exist_ok=True)
         (out / f"{w}.json").write_text(json.dumps(d, indent=1) + "\n")
         traffic[w] = {"hbm_bytes_per_launch": d["derived"]["hbm_bytes_per_launch"],
-                      "source": f"profiles/{rnd}/pmc/{w}.json (FETCH_SIZE x2 + WRITE_SIZE, KiB->B)"}
+                      "valu_busy": d["derived"]["valu_busy"],
+                      "source": f"profiles/{rnd}/pmc/{w}.json (FETCH_SIZE x2 + WRITE_SIZE, KiB->B; "
+                                f"valu_busy = SQ_INSTS_VALU x 4 / (1024 SIMDs x SQ_BUSY_CYCLES / 32))"}
         print(w, json.dumps(d["derived"], indent=1))
     traffic_f.write_text(json.dumps(traffic, indent=1) + "\n")
 
