@@ -41,7 +41,8 @@ typedef enum rg_status {
     RG_ERR_TEXTURE = -6,            /* texture index out of range / empty image (material.rs:34-47) */
     RG_ERR_DEVICE = -10,            /* HIP runtime error */
     RG_ERR_OUT_OF_MEMORY = -11,
-    RG_ERR_CANCELLED = -12          /* streaming receiver dropped         rendering.rs:53-54 */
+    RG_ERR_CANCELLED = -12,         /* streaming receiver dropped         rendering.rs:53-54 */
+    RG_ERR_COLLECTIVE = -13         /* rg_render_multi: RCCL missing or a collective failed */
 } rg_status;
 
 /* ------------------------------------------------------------------------
@@ -164,9 +165,24 @@ rg_status rg_scene_set_max_depth(rg_scene *scene, uint32_t max_recursion_depth);
 
 /* Blocking whole-frame render into a caller-owned host buffer of
  * width*height*4 bytes (row-major RGBA8, alpha 255).
- * Replaces rendering::render_image (rendering.rs:24-38). `stats` may be NULL. */
+ * Replaces rendering::render_image (rendering.rs:24-38). `stats` may be NULL.
+ * The frame renders in row bands whose device-to-host copies overlap the
+ * later bands' renders; a pinned `rgba_out` (rg_host_register, or memory from
+ * hipHostMalloc) receives the DMA directly, a pageable one through pinned
+ * staging.  Any max_recursion_depth renders (scene.rs:16 is a u32): depths
+ * above 65 keep their shading frames in device memory.  On a device error
+ * (RG_ERR_AABB_NORMAL / _NAN_DISTANCE / _TRANSMISSION: the reference's
+ * panics) the frame is still delivered and stats->error_pixel names the first
+ * (lowest-index) pixel that raised it. */
 rg_status rg_render_image(const rg_scene *scene, uint32_t width, uint32_t height,
                           uint8_t *rgba_out, rg_stats *stats);
+
+/* Page-lock a caller buffer (hipHostRegister) so rg_render_image / rg_render_tiles
+ * / rg_render_multi DMA straight into it; unregister before freeing it.  Optional:
+ * pageable buffers work too (staged).  A Rust caller registers its
+ * ImageBuffer's Vec once and reuses it across frames. */
+rg_status rg_host_register(void *ptr, size_t bytes);
+rg_status rg_host_unregister(void *ptr);
 
 /* Device-resident variant used by sharded / benchmark callers: renders the
  * tiles selected by `tiling` into `rgba_dev` (device pointer on the scene's
@@ -182,6 +198,17 @@ rg_status rg_render_image(const rg_scene *scene, uint32_t width, uint32_t height
 rg_status rg_render_tiles_async(const rg_scene *scene, uint32_t width, uint32_t height,
                                 const rg_tiling *tiling, uint8_t *rgba_dev, float *rgb_dev,
                                 void *stream, rg_stats *stats);
+
+/* Forget the launch state of `stream` (before the caller destroys that stream);
+ * the null stream's state lives as long as the scene. */
+rg_status rg_scene_release_stream(rg_scene *scene, void *stream);
+
+/* Status of the launches enqueued on `stream` since the previous call:
+ * synchronises the stream, returns the first (lowest-pixel) device error any
+ * of them raised (RG_OK if none) with its pixel in *error_pixel (nullable;
+ * -1 if none), and clears it.  For asynchronous callers (stats == NULL),
+ * whose launches otherwise report nothing. */
+rg_status rg_stream_status(const rg_scene *scene, void *stream, int32_t *error_pixel);
 
 /* Host-buffer variant of rg_render_tiles_async (blocking).  rgb_out nullable. */
 rg_status rg_render_tiles(const rg_scene *scene, uint32_t width, uint32_t height,
@@ -208,6 +235,23 @@ rg_status rg_render_stream(const rg_scene *scene, uint32_t width, uint32_t heigh
  * hit distance and body[i] the body index, or body[i] = -1 on a miss. */
 rg_status rg_trace(const rg_scene *scene, const double *rays, uint32_t n,
                    double *dist, int32_t *body);
+
+/* Single-process multi-GPU render (SURVEY.md §8(b),(e)): the same frame as
+ * rg_render_image, split over `ngpus` devices -- the scene's device first,
+ * then the next visible devices in order -- in `tile_rows`-row tiles dealt
+ * round-robin (tile t -> device t % ngpus; 0 = 8 rows).  Each device renders
+ * its tiles with its own replica of the scene (made on first use and kept),
+ * ONE RCCL ncclGather over xGMI brings the equal-size parts to the scene's
+ * device, which re-interleaves them into the frame; the frame is then copied
+ * to `rgba_out` (width*height*4 bytes, host).  The communicators come from
+ * ncclCommInitAll in this process (RCCL is loaded at run time: the librccl
+ * already in the process, else $RG_RCCL_LIBRARY, else librccl.so.1);
+ * RG_ERR_COLLECTIVE if it cannot be loaded.  No torch, no launcher: the
+ * drop-in for the reference's one blocking call (rendering.rs:24-38,
+ * src/render.rs:55) on a whole node.  `stats` sums the devices' rays;
+ * kernel_ms spans render + gather + assembly. */
+rg_status rg_render_multi(const rg_scene *scene, uint32_t width, uint32_t height, int32_t ngpus,
+                          uint32_t tile_rows, uint8_t *rgba_out, rg_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,12 @@ rg_status rg_debug_set_lane_depth(rg_scene *scene, int32_t min_depth);
  * path only.  Results are identical either way. */
 rg_status rg_debug_set_tile_order(rg_scene *scene, int32_t mode);
 
+/* Host-visible frames (rg_render_image / rg_render_tiles with a whole-frame
+ * tiling): render in this many row bands, each band's device-to-host copy
+ * overlapping the next bands' renders (1..16; 0 = by frame size, ~2 Mpx per
+ * band, at most 4).  Results are identical for every value. */
+rg_status rg_debug_set_image_bands(rg_scene *scene, int32_t bands);
+
 /* Copy the scene's 16 statistics words after the last render: [0..2] ray
  * counts, [4..8] BVH traversal statistics when the library was built with
  * -DRG_BVH_STATS (zero otherwise). */

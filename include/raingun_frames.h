@@ -41,15 +41,22 @@ void rg_frames_destroy(rg_frames *frames);
 /* Enqueue one frame (asynchronous: returns once its work is on the streams). */
 rg_status rg_frames_step(rg_frames *frames);
 
-/* Block until every enqueued frame is rendered, gathered and assembled. */
+/* Block until every enqueued frame is rendered, gathered and assembled.
+ * Returns the first device error (RG_ERR_AABB_NORMAL, _NAN_DISTANCE,
+ * _TRANSMISSION: the reference's panics) any of this rank's frames raised
+ * so far, RG_OK if none; the frames are still delivered. */
 rg_status rg_frames_flush(rg_frames *frames);
+
+/* rg_frames_flush, plus the pixel of that first error (-1 if none). */
+rg_status rg_frames_status(rg_frames *frames, int32_t *error_pixel);
 
 /* Rank 0: device pointer of the latest frame's assembled image (height rows of
  * width RGBA8 pixels, row-major), valid after rg_frames_flush; NULL elsewhere. */
 const uint8_t *rg_frames_image(const rg_frames *frames);
 
 /* Rank 0: copy the latest assembled image to host memory (height*width*4
- * bytes); blocks until every enqueued frame is done. */
+ * bytes); blocks until every enqueued frame is done.  Returns what
+ * rg_frames_flush returns (the image is copied either way). */
 rg_status rg_frames_read_image(const rg_frames *frames, uint8_t *host_out);
 
 #ifdef __cplusplus

@@ -24,6 +24,7 @@ RG_ERR_TEXTURE = -6
 RG_ERR_DEVICE = -10
 RG_ERR_OUT_OF_MEMORY = -11
 RG_ERR_CANCELLED = -12
+RG_ERR_COLLECTIVE = -13
 
 BODY_SPHERE, BODY_PLANE, BODY_DISK, BODY_AABB = 0, 1, 2, 3
 COLORATION_COLOR, COLORATION_TEXTURE = 0, 1
@@ -128,13 +129,18 @@ EXPORTED_SYMBOLS = (
     "rg_tiling_rows",
     "rg_render_stream",
     "rg_trace",
+    "rg_host_register",
+    "rg_host_unregister",
+    "rg_scene_release_stream",
+    "rg_stream_status",
+    "rg_render_multi",
 )
 # include/raingun_debug.h
 DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
-                 "rg_debug_set_tile_order", "rg_debug_set_lane_depth")
+                 "rg_debug_set_tile_order", "rg_debug_set_lane_depth", "rg_debug_set_image_bands")
 # include/raingun_frames.h
 FRAMES_SYMBOLS = ("rg_frames_create", "rg_frames_destroy", "rg_frames_step", "rg_frames_flush", "rg_frames_image",
-                  "rg_frames_read_image")
+                  "rg_frames_read_image", "rg_frames_status")
 PATH_AUTO, PATH_LIGHT, PATH_HEAVY = -1, 0, 1
 
 
@@ -185,6 +191,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_set_tile_order.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_set_lane_depth.restype = C.c_int32
     lib.rg_debug_set_lane_depth.argtypes = [C.c_void_p, C.c_int32]
+    lib.rg_debug_set_image_bands.restype = C.c_int32
+    lib.rg_debug_set_image_bands.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_counters.restype = C.c_int32
     lib.rg_debug_counters.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.rg_frames_create.restype = C.c_int32
@@ -202,6 +210,19 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_frames_read_image.argtypes = [C.c_void_p, C.c_void_p]
     lib.rg_trace.restype = C.c_int32
     lib.rg_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+    lib.rg_host_register.restype = C.c_int32
+    lib.rg_host_register.argtypes = [C.c_void_p, C.c_size_t]
+    lib.rg_host_unregister.restype = C.c_int32
+    lib.rg_host_unregister.argtypes = [C.c_void_p]
+    lib.rg_scene_release_stream.restype = C.c_int32
+    lib.rg_scene_release_stream.argtypes = [C.c_void_p, C.c_void_p]
+    lib.rg_stream_status.restype = C.c_int32
+    lib.rg_stream_status.argtypes = [C.c_void_p, C.c_void_p, P(C.c_int32)]
+    lib.rg_render_multi.restype = C.c_int32
+    lib.rg_render_multi.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int32, C.c_uint32, C.c_void_p,
+                                    P(rg_stats)]
+    lib.rg_frames_status.restype = C.c_int32
+    lib.rg_frames_status.argtypes = [C.c_void_p, P(C.c_int32)]
 
 
 def lib() -> C.CDLL:
@@ -234,3 +255,23 @@ def status_string(status: int) -> str:
 def check(status: int, what: str = "") -> None:
     if status != RG_OK:
         raise RaingunError(status, what)
+
+
+class HostRegistration:
+    """Page-lock a numpy array for direct DMA (rg_host_register) while in scope."""
+
+    def __init__(self, arr):
+        self.arr = arr
+        check(lib().rg_host_register(arr.ctypes.data, arr.nbytes), "rg_host_register")
+
+    def close(self) -> None:
+        if self.arr is not None:
+            lib().rg_host_unregister(self.arr.ctypes.data)
+            self.arr = None
+
+    def __enter__(self):
+        return self.arr
+
+    def __exit__(self, *exc):
+        self.close()
+

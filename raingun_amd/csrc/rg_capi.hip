@@ -1,13 +1,18 @@
 // rg_capi.hip — host side of libraingun_hip.so: the C ABI declared in
 // include/raingun.h.  Scene upload (SoA hot tables + cold shading tables),
-// tiled launches, ray counters, device error word, streaming bands and the
-// batch closest-hit query.  No exception or abort crosses the ABI.
+// tiled launches, ray counters, device error words, the host-visible image
+// path (banded renders overlapped with their device-to-host copies),
+// streaming bands and the batch closest-hit query.  The single-process
+// multi-GPU entry (rg_render_multi) is in rg_multi.hip.  No exception or
+// abort crosses the ABI.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <vector>
 
@@ -15,73 +20,29 @@
 #include "../../include/raingun_debug.h"
 #include "rg_bvh.h"
 #include "rg_device.h"
+#include "rg_internal.h"
 
 #pragma clang fp contract(off)
 
 #ifndef RG_BVH_MIN_SPHERES
 #define RG_BVH_MIN_SPHERES 16  // below this a scan of the sphere table is as cheap as a traversal
 #endif
+#ifndef RG_LANE_MIN_DEPTH
+#define RG_LANE_MIN_DEPTH 1
+#endif
+#ifndef RG_TILE_ORDER
+#define RG_TILE_ORDER -1
+#endif
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream);
+extern "C" hipError_t rg_render_grid_threads(const RgKernelArgs *a, int maxd, size_t *threads);
+extern "C" int rg_max_array_frames(void);
 extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scratch, uint32_t *perm, hipStream_t stream);
 extern "C" size_t rg_tile_order_scratch_words(uint32_t ntiles);
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,
                                       int32_t *body, hipStream_t stream);
 
-// Per-stream launch state (ray counters, tile-queue heads, error word, tile
-// ordering scratch, timing events).  Launches on distinct streams may run
-// concurrently (frames in flight), so they must not share it; launches on one
-// stream are ordered by the stream and reuse it.
-struct rg_launch_ctx {
-    hipStream_t stream = nullptr;
-    unsigned long long *counters = nullptr;  // RG_COUNTER_WORDS words (rg_device.h)
-    uint32_t *tile_cost = nullptr, *tile_perm = nullptr;  // probe/sort scratch (rg_launch_tile_order), order
-    size_t tile_cap = 0;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-};
-
-struct rg_scene {
-    int device = 0;
-    double fov = 90.0;
-    float def[3] = {0, 0, 0};
-    uint32_t max_depth = 10;
-    int32_t n_sph = 0, n_pln = 0, n_dsk = 0, n_box = 0, n_bodies = 0, n_lights = 0, n_textures = 0;
-    std::vector<void *> allocations;
-    RgSph *sph = nullptr;
-    double *sph_cc = nullptr;
-    RgSphF *sphf = nullptr;
-    RgSphF2 *sphf2 = nullptr;
-    int32_t path = RG_PATH_AUTO;
-    int32_t *sph_id = nullptr, *pln_id = nullptr, *dsk_id = nullptr, *box_id = nullptr;
-    RgPln *pln = nullptr;
-    RgDsk *dsk = nullptr;
-    RgBox *box = nullptr;
-    RgBodyDev *bodies = nullptr;
-    RgMatDev *mats = nullptr;
-    RgLightDev *lights = nullptr;
-    RgTexDev *texs = nullptr;
-    RgBvhNode *nodes = nullptr;  // sphere BVH (sphere tables are in its leaf order)
-    int32_t n_nodes = 0;
-    int32_t lane_stack = 0;      // per-lane walk stack entries the tree needs (0: per-lane walk unavailable)
-#ifndef RG_LANE_MIN_DEPTH
-#define RG_LANE_MIN_DEPTH 1
-#endif
-    int32_t lane_min_depth = RG_LANE_MIN_DEPTH;  // rays of this depth and deeper walk the BVH per lane
-    bool bvh_enabled = true;
-    float bvh_obound = 0.0f;
-    double bvh_rbound = 0.0, bvh_margin = 0.0, bvh_extent = 0.0;
-    rg_bvh_info bvh_info{};
-    mutable std::vector<rg_launch_ctx *> ctxs;  // one per stream used
-    mutable rg_launch_ctx *last = nullptr;       // the context of the latest launch (rg_debug_counters)
-#ifndef RG_TILE_ORDER
-#define RG_TILE_ORDER -1
-#endif
-    int tile_order = RG_TILE_ORDER;  // expensive tiles first (rg_kernels.hip "tile ordering"): -1 auto (heavy path), 0, 1
-};
-
 namespace {
-
-constexpr int kMaxFrames = 64;  // largest compiled frame stack (rg_launch_render)
 
 bool ok(hipError_t e) { return e == hipSuccess; }
 
@@ -125,19 +86,48 @@ void make_filter_records(const double *p, RgSphF &f, RgSphF2 &f2) {
 // f64::to_radians (2017 std: self * (PI / 180)), then libm tan (ray.rs:45).
 double fov_adjustment(double fov) { return std::tan(fov * (3.14159265358979323846 / 180.0) / 2.0); }
 
+// Parameters the body tests read (bodies.rs): sphere 4, plane 6, disk 7, AABB 6.
+int body_params(uint32_t kind) { return kind == RG_BODY_SPHERE ? 4 : kind == RG_BODY_DISK ? 7 : 6; }
+
+// A body or light parameter that is non-finite or >= 1e100 in magnitude: ray
+// arithmetic may then overflow to NaN distances (rg_kernels.hip ray_exotic).
+bool exotic_value(double v) { return !(std::fabs(v) < 1e100); }
+
+void destroy_ctx(rg_launch_ctx *c) {
+    if (c->counters) (void)hipFree(c->counters);
+    if (c->sticky) (void)hipFree(c->sticky);
+    if (c->tile_cost) (void)hipFree(c->tile_cost);
+    if (c->tile_perm) (void)hipFree(c->tile_perm);
+    if (c->deep) (void)hipFree(c->deep);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    delete c;
+}
+
+void release_image_res(rg_image_res &r) {
+    for (hipStream_t &st : r.rs)
+        if (st) { (void)hipStreamSynchronize(st); (void)hipStreamDestroy(st); st = nullptr; }
+    if (r.cs) { (void)hipStreamSynchronize(r.cs); (void)hipStreamDestroy(r.cs); r.cs = nullptr; }
+    for (hipEvent_t &e : r.ev_done) if (e) { (void)hipEventDestroy(e); e = nullptr; }
+    for (hipEvent_t &e : r.ev_copy) if (e) { (void)hipEventDestroy(e); e = nullptr; }
+    for (hipEvent_t *e : {&r.ev_t0, &r.ev_t1, &r.ev_join})
+        if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
+    if (r.d_rgba) (void)hipFree(r.d_rgba);
+    if (r.d_rgb) (void)hipFree(r.d_rgb);
+    if (r.h_stage) (void)hipHostFree(r.h_stage);
+    if (r.h_snap) (void)hipHostFree(r.h_snap);
+    r = rg_image_res{};
+}
+
 void release(rg_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
+    rg_multi_release(s);
+    release_image_res(s->img);
     for (void *p : s->allocations) (void)hipFree(p);
     s->allocations.clear();
-    for (rg_launch_ctx *c : s->ctxs) {
-        if (c->counters) (void)hipFree(c->counters);
-        if (c->tile_cost) (void)hipFree(c->tile_cost);
-        if (c->tile_perm) (void)hipFree(c->tile_perm);
-        if (c->ev0) (void)hipEventDestroy(c->ev0);
-        if (c->ev1) (void)hipEventDestroy(c->ev1);
-        delete c;
-    }
+    for (rg_launch_ctx *c : s->ctxs) destroy_ctx(c);
+    s->ctxs.clear();
     delete s;
 }
 
@@ -148,20 +138,42 @@ rg_launch_ctx *ctx_for(const rg_scene *s, hipStream_t stream) {
     rg_launch_ctx *c = new (std::nothrow) rg_launch_ctx();
     if (!c) return nullptr;
     c->stream = stream;
-    void *p = nullptr;
+    void *p = nullptr, *q = nullptr;
     if (!ok(hipMalloc(&p, RG_COUNTER_WORDS * sizeof(unsigned long long)))) { delete c; return nullptr; }
     c->counters = static_cast<unsigned long long *>(p);
+    if (!ok(hipMalloc(&q, sizeof(unsigned long long))) || !ok(hipMemset(q, 0, sizeof(unsigned long long)))) {
+        if (q) (void)hipFree(q);
+        destroy_ctx(c);
+        return nullptr;
+    }
+    c->sticky = static_cast<unsigned long long *>(q);
     if (!ok(hipEventCreate(&c->ev0)) || !ok(hipEventCreate(&c->ev1))) {
-        (void)hipFree(c->counters);
-        if (c->ev0) (void)hipEventDestroy(c->ev0);
-        delete c;
+        destroy_ctx(c);
         return nullptr;
     }
     s->ctxs.push_back(c);
     return c;
 }
 
-RgKernelArgs make_args(const rg_scene *s) {
+bool tiling_valid(const rg_tiling *t) {
+    return t && t->tile_rows > 0 && t->tile_stride > 0 && t->tile_offset < t->tile_stride;
+}
+
+int frames_needed(uint32_t max_depth) { return max_depth > 1 ? (int)max_depth - 1 : 1; }
+
+// decode the complemented error key of counters[3] / a sticky word
+rg_status decode_error(unsigned long long word, int32_t *pixel) {
+    if (word == 0) return RG_OK;
+    const unsigned long long key = ~word;
+    if (pixel) *pixel = (int32_t)(key >> 8);
+    return (rg_status)(-(int32_t)(key & 0xff));
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- internal (rg_internal.h)
+
+RgKernelArgs rg_make_args(const rg_scene *s) {
     RgKernelArgs a;
     std::memset(&a, 0, sizeof a);
     a.sph = s->sph;
@@ -197,6 +209,7 @@ RgKernelArgs make_args(const rg_scene *s) {
     a.n_bodies = s->n_bodies;
     a.n_lights = s->n_lights;
     a.n_textures = s->n_textures;
+    a.nan_scene = s->nan_scene ? 1 : 0;
     // per-lane BVH walk (heavy path only): stacks of lane_stack entries per thread at LDS offset 0
     const bool lane = bvh && rg_heavy_path(a) && s->lane_stack > 0 && s->lane_min_depth < 1 << 20;
     a.lane_stack = lane ? s->lane_stack : 0;
@@ -226,13 +239,186 @@ RgKernelArgs make_args(const rg_scene *s) {
     return a;
 }
 
-bool tiling_valid(const rg_tiling *t) {
-    return t && t->tile_rows > 0 && t->tile_stride > 0 && t->tile_offset < t->tile_stride;
+rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
+                          uint8_t *rgba_dev, float *rgb_dev, hipStream_t st, unsigned long long *snap,
+                          rg_launch_ctx **ctx_out, bool timed) {
+    if (!s || !rgba_dev || width == 0 || height == 0 || !tiling_valid(tiling)) return RG_ERR_INVALID_ARGUMENT;
+    if (width < height) return RG_ERR_PORTRAIT;  // ray.rs:42
+    const uint32_t out_rows = rg_tiling_rows(height, tiling);
+    if ((unsigned long long)out_rows * width >= (1ull << 32) || (unsigned long long)height * width >= (1ull << 32))
+        return RG_ERR_INVALID_ARGUMENT;  // the reference's u32 pixel index (rendering.rs:27)
+    if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
+    rg_launch_ctx *cx = ctx_for(s, st);
+    if (!cx) return RG_ERR_OUT_OF_MEMORY;
+    s->last = cx;
+    if (ctx_out) *ctx_out = cx;
+    RgKernelArgs a = rg_make_args(s);
+    a.counters = cx->counters;
+    a.err_sticky = cx->sticky;
+    a.width = width;
+    a.height = height;
+    a.tile_rows = tiling->tile_rows;
+    a.tile_stride = tiling->tile_stride;
+    a.tile_offset = tiling->tile_offset;
+    a.out_rows = out_rows;
+    a.aspect = (double)width / (double)height;
+    a.rgba = reinterpret_cast<uint32_t *>(rgba_dev);
+    a.rgb = rgb_dev;
+    const int frames = frames_needed(s->max_depth);
+    if (frames > rg_max_array_frames() && out_rows > 0) {
+        // deep recursion: frames in a global buffer sized for this launch's (persistent) grid
+        size_t threads = 0;
+        if (!ok(rg_render_grid_threads(&a, frames, &threads)) || threads == 0 || threads > 0xFFFFFFFFull)
+            return RG_ERR_DEVICE;
+        const size_t bytes = threads * (size_t)frames * RG_FRAME_BYTES;
+        if (bytes > cx->deep_bytes) {
+            if (cx->deep) (void)hipFree(cx->deep);
+            cx->deep = nullptr;
+            cx->deep_bytes = 0;
+            if (!ok(hipMalloc(&cx->deep, bytes))) { (void)hipGetLastError(); cx->deep = nullptr; return RG_ERR_OUT_OF_MEMORY; }
+            cx->deep_bytes = bytes;
+        }
+        a.deep_stack = cx->deep;
+        a.deep_stride = (uint32_t)threads;
+    }
+    if (!ok(hipMemsetAsync(cx->counters, 0, RG_COUNTER_WORDS * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
+    if (timed && !ok(hipEventRecord(cx->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
+    if (s->tile_order == 1 || (s->tile_order < 0 && rg_heavy_path(a))) {
+        const size_t ntiles = (size_t)((width + 7u) / 8u) * ((out_rows + 7u) / 8u);
+        if (ntiles > cx->tile_cap) {
+            if (cx->tile_cost) (void)hipFree(cx->tile_cost);
+            if (cx->tile_perm) (void)hipFree(cx->tile_perm);
+            cx->tile_cost = cx->tile_perm = nullptr;
+            cx->tile_cap = 0;
+            if (!ok(hipMalloc(&cx->tile_cost, rg_tile_order_scratch_words((uint32_t)ntiles) * 4)) ||
+                !ok(hipMalloc(&cx->tile_perm, ntiles * 4)))
+                return RG_ERR_OUT_OF_MEMORY;
+            cx->tile_cap = ntiles;
+        }
+        if (ntiles > 0) {
+            if (!ok(rg_launch_tile_order(&a, cx->tile_cost, cx->tile_perm, st))) return RG_ERR_DEVICE;
+            a.tile_perm = cx->tile_perm;
+        }
+    }
+    if (out_rows > 0 && !ok(rg_launch_render(&a, frames, st))) return RG_ERR_DEVICE;
+    if (timed && !ok(hipEventRecord(cx->ev1, st))) return RG_ERR_DEVICE;
+    if (snap && !ok(hipMemcpyAsync(snap, cx->counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st)))
+        return RG_ERR_DEVICE;
+    return RG_OK;
 }
 
-int frames_needed(uint32_t max_depth) { return max_depth > 1 ? (int)max_depth - 1 : 1; }
+rg_status rg_snap_status(const unsigned long long *snap, rg_stats *stats) {
+    if (stats) {
+        stats->rays.primary = snap[0];
+        stats->rays.shadow = snap[1];
+        stats->rays.secondary = snap[2];
+        stats->error_pixel = -1;
+    }
+    return decode_error(snap[3], stats ? &stats->error_pixel : nullptr);
+}
+
+bool rg_host_is_pinned(const void *p, size_t bytes) {
+    if (!p || bytes == 0) return false;
+    auto one = [](const void *q) {
+        hipPointerAttribute_t at;
+        std::memset(&at, 0, sizeof at);
+        if (hipPointerGetAttributes(&at, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return at.type == hipMemoryTypeHost;
+    };
+    return one(p) && one(static_cast<const char *>(p) + bytes - 1);
+}
+
+namespace {
+
+// Host tables of a scene: everything rg_scene_create uploads, kept so that
+// rg_render_multi can place replicas on other devices.
+rg_status upload_tables(rg_scene *s, const rg_host_tables &h) {
+    rg_status st = RG_OK;
+#define RG_UP(dst, vec) \
+    if (st == RG_OK) st = upload(s, &s->dst, h.vec.data(), h.vec.size())
+    RG_UP(sph, sph);
+    RG_UP(sph_cc, sph_cc);
+    RG_UP(sphf, sphf);
+    RG_UP(sphf2, sphf2);
+    RG_UP(sph_id, sph_id);
+    RG_UP(pln, pln);
+    RG_UP(pln_id, pln_id);
+    RG_UP(dsk, dsk);
+    RG_UP(dsk_id, dsk_id);
+    RG_UP(box, box);
+    RG_UP(box_id, box_id);
+    RG_UP(bodies, bodies);
+    RG_UP(mats, mats);
+    RG_UP(lights, lights);
+    RG_UP(nodes, nodes);
+#undef RG_UP
+    // textures: RGBA8 -> one u32 per texel (one 4-byte gather per lookup)
+    std::vector<RgTexDev> texs(h.tex_w.size());
+    for (size_t i = 0; st == RG_OK && i < texs.size(); ++i) {
+        texs[i].w = (int32_t)h.tex_w[i];
+        texs[i].h = (int32_t)h.tex_h[i];
+        texs[i].texels = nullptr;
+        if (h.texels[i].empty()) continue;
+        uint32_t *dp = nullptr;
+        st = upload(s, &dp, h.texels[i].data(), h.texels[i].size());
+        texs[i].texels = dp;
+    }
+    if (st == RG_OK) st = upload(s, &s->texs, texs.data(), texs.size());
+    return st;
+}
+
+void copy_scalars(rg_scene *dst, const rg_scene *src) {
+    dst->fov = src->fov;
+    std::memcpy(dst->def, src->def, sizeof dst->def);
+    dst->max_depth = src->max_depth;
+    dst->n_sph = src->n_sph;
+    dst->n_pln = src->n_pln;
+    dst->n_dsk = src->n_dsk;
+    dst->n_box = src->n_box;
+    dst->n_bodies = src->n_bodies;
+    dst->n_lights = src->n_lights;
+    dst->n_textures = src->n_textures;
+    dst->n_nodes = src->n_nodes;
+    dst->lane_stack = src->lane_stack;
+    dst->nan_scene = src->nan_scene;
+    dst->bvh_obound = src->bvh_obound;
+    dst->bvh_rbound = src->bvh_rbound;
+    dst->bvh_margin = src->bvh_margin;
+    dst->bvh_extent = src->bvh_extent;
+    dst->bvh_info = src->bvh_info;
+}
 
 }  // namespace
+
+rg_status rg_scene_replica(const rg_scene *src, int32_t device, rg_scene **out) {
+    *out = nullptr;
+    if (!src->host) return RG_ERR_INVALID_ARGUMENT;
+    rg_scene *s = new (std::nothrow) rg_scene();
+    if (!s) return RG_ERR_OUT_OF_MEMORY;
+    s->device = device;
+    copy_scalars(s, src);
+    rg_sync_settings(s, src);
+    s->host = src->host;
+    if (!ok(hipSetDevice(device))) { release(s); return RG_ERR_DEVICE; }
+    rg_status st = upload_tables(s, *src->host);
+    if (st == RG_OK && !(s->last = ctx_for(s, nullptr))) st = RG_ERR_OUT_OF_MEMORY;
+    if (st != RG_OK) { release(s); return st; }
+    *out = s;
+    return RG_OK;
+}
+
+void rg_scene_free(rg_scene *s) { release(s); }
+
+void rg_sync_settings(rg_scene *dst, const rg_scene *src) {
+    dst->max_depth = src->max_depth;
+    dst->path = src->path;
+    dst->bvh_enabled = src->bvh_enabled;
+    dst->lane_min_depth = src->lane_min_depth;
+    dst->tile_order = src->tile_order;
+}
 
 extern "C" {
 
@@ -250,6 +436,7 @@ const char *rg_status_string(int32_t st) {
     case RG_ERR_DEVICE: return "HIP runtime error";
     case RG_ERR_OUT_OF_MEMORY: return "out of device memory";
     case RG_ERR_CANCELLED: return "cancelled by the tile callback";
+    case RG_ERR_COLLECTIVE: return "RCCL unavailable or failed (rg_render_multi)";
     default: return "unknown status";
     }
 }
@@ -275,6 +462,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return RG_ERR_DEVICE;
     // validate enums and textures on the host first
+    bool nan_scene = false;
     for (uint32_t i = 0; i < d->n_bodies; ++i) {
         const rg_body &b = d->bodies[i];
         if (b.kind > RG_BODY_AABB || b.material.coloration > RG_COLORATION_TEXTURE ||
@@ -286,37 +474,36 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
                 d->textures[t].height == 0 || d->textures[t].width > 0x7fffffffu || d->textures[t].height > 0x7fffffffu)
                 return RG_ERR_TEXTURE;
         }
+        for (int k = 0; k < body_params(b.kind); ++k) nan_scene |= exotic_value(b.p[k]);
     }
-    for (uint32_t i = 0; i < d->n_lights; ++i)
+    for (uint32_t i = 0; i < d->n_lights; ++i) {
         if (d->lights[i].kind > RG_LIGHT_SPHERICAL) return RG_ERR_INVALID_ARGUMENT;
+        for (int k = 0; k < 3; ++k) nan_scene |= exotic_value(d->lights[i].v[k]);
+    }
 
     rg_scene *s = new (std::nothrow) rg_scene();
     if (!s) return RG_ERR_OUT_OF_MEMORY;
+    std::shared_ptr<rg_host_tables> hp(new (std::nothrow) rg_host_tables());
+    if (!hp) { delete s; return RG_ERR_OUT_OF_MEMORY; }
+    rg_host_tables &h = *hp;
     s->device = device;
     s->fov = d->fov;
     std::memcpy(s->def, d->default_color, sizeof s->def);
     s->max_depth = d->max_recursion_depth;
+    s->nan_scene = nan_scene;
     if (!ok(hipSetDevice(device))) { release(s); return RG_ERR_DEVICE; }
 
-    std::vector<RgSph> sph;
     std::vector<double> sph_raw;  // center xyz, radius (BVH build input)
-    std::vector<RgSphF> sphf;
-    std::vector<RgSphF2> sphf2;
-    std::vector<double> sph_cc;
-    std::vector<int32_t> sph_id, pln_id, dsk_id, box_id;
-    std::vector<RgPln> pln;
-    std::vector<RgDsk> dsk;
-    std::vector<RgBox> box;
-    std::vector<RgBodyDev> bodies(d->n_bodies);
-    std::vector<RgMatDev> mats(d->n_bodies);
+    h.bodies.resize(d->n_bodies);
+    h.mats.resize(d->n_bodies);
     for (uint32_t i = 0; i < d->n_bodies; ++i) {
         const rg_body &b = d->bodies[i];
         const double *p = b.p;
-        bodies[i].kind = (int32_t)b.kind;
-        bodies[i].pad = 0;
-        std::memcpy(bodies[i].p, b.p, sizeof bodies[i].p);
+        h.bodies[i].kind = (int32_t)b.kind;
+        h.bodies[i].pad = 0;
+        std::memcpy(h.bodies[i].p, b.p, sizeof h.bodies[i].p);
         const rg_material &m = b.material;
-        RgMatDev &md = mats[i];
+        RgMatDev &md = h.mats[i];
         md.coloration = (int32_t)m.coloration;
         std::memcpy(md.color, m.color, sizeof md.color);
         md.tex = m.texture;
@@ -331,41 +518,43 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         case RG_BODY_SPHERE:
             // r2 = radius * radius and cc = (c.c) evaluated exactly as the per-ray
             // reference expressions (bodies.rs:95,97) -> bit-identical.
-            sph.push_back(RgSph{p[0], p[1], p[2], p[3] * p[3]});
-            sphf.emplace_back();
-            sphf2.emplace_back();
-            make_filter_records(p, sphf.back(), sphf2.back());
-            sph_cc.push_back(dot3(p, p));  // padded to an even count after the loop
-            sph_id.push_back((int32_t)i);
+            h.sph.push_back(RgSph{p[0], p[1], p[2], p[3] * p[3]});
+            h.sphf.emplace_back();
+            h.sphf2.emplace_back();
+            make_filter_records(p, h.sphf.back(), h.sphf2.back());
+            h.sph_cc.push_back(dot3(p, p));  // padded to an even count after the loop
+            h.sph_id.push_back((int32_t)i);
             sph_raw.insert(sph_raw.end(), p, p + 4);
             break;
         case RG_BODY_PLANE:
-            pln.push_back(RgPln{p[0], p[1], p[2], p[3], p[4], p[5], dot3(p, p + 3), 0.0});
-            pln_id.push_back((int32_t)i);
+            h.pln.push_back(RgPln{p[0], p[1], p[2], p[3], p[4], p[5], dot3(p, p + 3), 0.0});
+            h.pln_id.push_back((int32_t)i);
             break;
         case RG_BODY_DISK:
-            dsk.push_back(RgDsk{p[0], p[1], p[2], p[3], p[4], p[5], p[6], dot3(p, p + 3)});
-            dsk_id.push_back((int32_t)i);
+            h.dsk.push_back(RgDsk{p[0], p[1], p[2], p[3], p[4], p[5], p[6], dot3(p, p + 3)});
+            h.dsk_id.push_back((int32_t)i);
             break;
         default:
-            box.push_back(RgBox{{p[0], p[1], p[2]}, {p[3], p[4], p[5]}});
-            box_id.push_back((int32_t)i);
+            h.box.push_back(RgBox{{p[0], p[1], p[2]}, {p[3], p[4], p[5]}});
+            h.box_id.push_back((int32_t)i);
             break;
         }
     }
     // Sphere BVH: reorder the sphere tables into leaf order (sph_id keeps the
-    // YAML index, so the closest-hit tie-break is unaffected).
+    // YAML index, so the closest-hit tie-break is unaffected).  Not for scenes
+    // whose arithmetic may produce NaN distances: the scene.rs:38 panic needs
+    // every ray's hit count, which a pruned traversal does not see.
     RgBvhBuild bvh;
-    if ((int)sph.size() >= RG_BVH_MIN_SPHERES && rg_build_bvh(sph_raw.data(), (int)sph.size(), bvh)) {
+    if (!nan_scene && (int)h.sph.size() >= RG_BVH_MIN_SPHERES && rg_build_bvh(sph_raw.data(), (int)h.sph.size(), bvh)) {
         auto permute = [&](auto &v) {
             auto old = v;
             for (size_t j = 0; j < bvh.order.size(); ++j) v[j] = old[bvh.order[j]];
         };
-        permute(sph);
-        permute(sphf);
-        permute(sphf2);
-        permute(sph_cc);
-        permute(sph_id);
+        permute(h.sph);
+        permute(h.sphf);
+        permute(h.sphf2);
+        permute(h.sph_cc);
+        permute(h.sph_id);
         s->bvh_obound = bvh.obound;
         s->bvh_rbound = bvh.rbound;
         s->bvh_margin = bvh.margin;
@@ -377,70 +566,53 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         s->bvh_info.lane_stack = bvh.lane_stack;
         s->bvh_info.margin = (float)bvh.margin;
         s->bvh_info.origin_bound = bvh.obound;
+        h.nodes = bvh.nodes;
     }
-    if (sph_cc.size() % 2) sph_cc.push_back(0.0);  // LDS staging copies 16-B units
-    std::vector<RgLightDev> lights(d->n_lights);
+    if (h.sph_cc.size() % 2) h.sph_cc.push_back(0.0);  // LDS staging copies 16-B units
+    h.lights.resize(d->n_lights);
     for (uint32_t i = 0; i < d->n_lights; ++i) {
         const rg_light &l = d->lights[i];
-        lights[i].kind = (int32_t)l.kind;
-        std::memcpy(lights[i].color, l.color, sizeof lights[i].color);
-        lights[i].intensity = l.intensity;
-        lights[i].pad = 0;
-        std::memcpy(lights[i].v, l.v, sizeof lights[i].v);
+        RgLightDev &ld = h.lights[i];
+        ld.kind = (int32_t)l.kind;
+        std::memcpy(ld.color, l.color, sizeof ld.color);
+        ld.intensity = l.intensity;
+        ld.pad = 0;
+        std::memcpy(ld.v, l.v, sizeof ld.v);
         // Directional: normalize(-direction) (lights.rs:48) is a per-light constant.
         // Same IEEE ops in the same order as the device would run -> identical bits.
         double nx = -l.v[0], ny = -l.v[1], nz = -l.v[2];
         double inv = 1.0 / std::sqrt((nx * nx + ny * ny) + nz * nz);
-        lights[i].dn[0] = nx * inv;
-        lights[i].dn[1] = ny * inv;
-        lights[i].dn[2] = nz * inv;
-        lights[i].pad2 = 0.0;
+        ld.dn[0] = nx * inv;
+        ld.dn[1] = ny * inv;
+        ld.dn[2] = nz * inv;
+        ld.pad2 = 0.0;
     }
-    s->n_sph = (int32_t)sph.size();
-    s->n_pln = (int32_t)pln.size();
-    s->n_dsk = (int32_t)dsk.size();
-    s->n_box = (int32_t)box.size();
+    h.tex_w.resize(d->n_textures);
+    h.tex_h.resize(d->n_textures);
+    h.texels.resize(d->n_textures);
+    for (uint32_t i = 0; i < d->n_textures; ++i) {
+        const rg_texture &t = d->textures[i];
+        h.tex_w[i] = t.width;
+        h.tex_h[i] = t.height;
+        const size_t n = (size_t)t.width * t.height;
+        if (n == 0 || !t.rgba) continue;
+        h.texels[i].resize(n);
+        std::memcpy(h.texels[i].data(), t.rgba, n * 4);
+    }
+    s->n_sph = (int32_t)h.sph.size();
+    s->n_pln = (int32_t)h.pln.size();
+    s->n_dsk = (int32_t)h.dsk.size();
+    s->n_box = (int32_t)h.box.size();
     s->n_bodies = (int32_t)d->n_bodies;
     s->n_lights = (int32_t)d->n_lights;
     s->n_textures = (int32_t)d->n_textures;
-
-    rg_status st = RG_OK;
-#define RG_UP(dst, vec) \
-    if (st == RG_OK) st = upload(s, &s->dst, vec.data(), vec.size())
-    RG_UP(sph, sph);
-    RG_UP(sph_cc, sph_cc);
-    RG_UP(sphf, sphf);
-    RG_UP(sphf2, sphf2);
-    RG_UP(sph_id, sph_id);
-    RG_UP(pln, pln);
-    RG_UP(pln_id, pln_id);
-    RG_UP(dsk, dsk);
-    RG_UP(dsk_id, dsk_id);
-    RG_UP(box, box);
-    RG_UP(box_id, box_id);
-    RG_UP(bodies, bodies);
-    RG_UP(mats, mats);
-    RG_UP(lights, lights);
-    RG_UP(nodes, bvh.nodes);
-#undef RG_UP
-    s->n_nodes = (int32_t)bvh.nodes.size();
+    s->n_nodes = (int32_t)h.nodes.size();
     // the stack entry keeps the node index in its low RG_LANE_NODE_BITS bits
     s->lane_stack = (s->n_nodes <= (1 << RG_LANE_NODE_BITS) && bvh.lane_stack <= RG_LANE_STACK_MAX)
                         ? std::max(bvh.lane_stack, 1) : 0;
-    // textures: RGBA8 -> one u32 per texel (one 4-byte gather per lookup)
-    std::vector<RgTexDev> texs(d->n_textures);
-    for (uint32_t i = 0; st == RG_OK && i < d->n_textures; ++i) {
-        const rg_texture &t = d->textures[i];
-        texs[i].w = (int32_t)t.width;
-        texs[i].h = (int32_t)t.height;
-        texs[i].texels = nullptr;
-        size_t n = (size_t)t.width * t.height;
-        if (n == 0 || !t.rgba) continue;
-        uint32_t *dp = nullptr;
-        st = upload(s, &dp, reinterpret_cast<const uint32_t *>(t.rgba), n);
-        texs[i].texels = dp;
-    }
-    if (st == RG_OK) st = upload(s, &s->texs, texs.data(), texs.size());
+
+    rg_status st = upload_tables(s, h);
+    s->host = hp;
     if (st == RG_OK && !(s->last = ctx_for(s, nullptr))) st = RG_ERR_OUT_OF_MEMORY;  // default-stream context
     if (st != RG_OK) { release(s); return st; }
     *out = s;
@@ -455,156 +627,343 @@ rg_status rg_scene_set_max_depth(rg_scene *s, uint32_t max_depth) {
     return RG_OK;
 }
 
+rg_status rg_scene_release_stream(rg_scene *s, void *stream) {
+    if (!s) return RG_ERR_INVALID_ARGUMENT;
+    hipStream_t hs = static_cast<hipStream_t>(stream);
+    if (!hs) return RG_OK;  // the null-stream context lives as long as the scene
+    if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
+    for (size_t i = 0; i < s->ctxs.size(); ++i) {
+        if (s->ctxs[i]->stream != hs) continue;
+        rg_launch_ctx *c = s->ctxs[i];
+        (void)hipStreamSynchronize(hs);
+        if (s->last == c) s->last = ctx_for(s, nullptr);
+        s->ctxs.erase(s->ctxs.begin() + (std::ptrdiff_t)i);
+        destroy_ctx(c);
+        break;
+    }
+    return RG_OK;
+}
+
+rg_status rg_stream_status(const rg_scene *s, void *stream, int32_t *error_pixel) {
+    if (!s) return RG_ERR_INVALID_ARGUMENT;
+    if (error_pixel) *error_pixel = -1;
+    if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
+    hipStream_t hs = static_cast<hipStream_t>(stream);
+    for (rg_launch_ctx *c : s->ctxs) {
+        if (c->stream != hs) continue;
+        unsigned long long w = 0;
+        if (!ok(hipStreamSynchronize(hs)) || !ok(hipMemcpy(&w, c->sticky, sizeof w, hipMemcpyDeviceToHost)) ||
+            !ok(hipMemset(c->sticky, 0, sizeof w)))
+            return RG_ERR_DEVICE;
+        return decode_error(w, error_pixel);
+    }
+    return RG_OK;  // nothing was launched on this stream
+}
+
 rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
                                 uint8_t *rgba_dev, float *rgb_dev, void *stream, rg_stats *stats) {
-    if (!s || !rgba_dev || width == 0 || height == 0 || !tiling_valid(tiling)) return RG_ERR_INVALID_ARGUMENT;
-    if (width < height) return RG_ERR_PORTRAIT;  // ray.rs:42
-    if (frames_needed(s->max_depth) > kMaxFrames) return RG_ERR_INVALID_ARGUMENT;
-    uint32_t out_rows = rg_tiling_rows(height, tiling);
-    if ((unsigned long long)out_rows * width >= (1ull << 32) || (unsigned long long)height * width >= (1ull << 32))
-        return RG_ERR_INVALID_ARGUMENT;  // the reference's u32 pixel index (rendering.rs:27)
-    if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    rg_launch_ctx *cx = ctx_for(s, st);
-    if (!cx) return RG_ERR_OUT_OF_MEMORY;
-    s->last = cx;
-    RgKernelArgs a = make_args(s);
-    a.counters = cx->counters;
-    a.width = width;
-    a.height = height;
-    a.tile_rows = tiling->tile_rows;
-    a.tile_stride = tiling->tile_stride;
-    a.tile_offset = tiling->tile_offset;
-    a.out_rows = out_rows;
-    a.aspect = (double)width / (double)height;
-    a.rgba = reinterpret_cast<uint32_t *>(rgba_dev);
-    a.rgb = rgb_dev;
-    if (!ok(hipMemsetAsync(cx->counters, 0, RG_COUNTER_WORDS * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
-    if (stats && !ok(hipEventRecord(cx->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
-    if (s->tile_order == 1 || (s->tile_order < 0 && rg_heavy_path(a))) {
-        const size_t ntiles = (size_t)((width + 7u) / 8u) * ((out_rows + 7u) / 8u);
-        if (ntiles > cx->tile_cap) {
-            if (cx->tile_cost) (void)hipFree(cx->tile_cost);
-            if (cx->tile_perm) (void)hipFree(cx->tile_perm);
-            cx->tile_cost = cx->tile_perm = nullptr;
-            cx->tile_cap = 0;
-            if (!ok(hipMalloc(&cx->tile_cost, rg_tile_order_scratch_words((uint32_t)ntiles) * 4)) ||
-                !ok(hipMalloc(&cx->tile_perm, ntiles * 4)))
-                return RG_ERR_OUT_OF_MEMORY;
-            cx->tile_cap = ntiles;
-        }
-        if (!ok(rg_launch_tile_order(&a, cx->tile_cost, cx->tile_perm, st))) return RG_ERR_DEVICE;
-        a.tile_perm = cx->tile_perm;
-    }
-    if (out_rows == 0) return RG_OK;
-    if (!ok(rg_launch_render(&a, frames_needed(s->max_depth), st))) return RG_ERR_DEVICE;
-    if (!stats) return RG_OK;
-    if (!ok(hipEventRecord(cx->ev1, st))) return RG_ERR_DEVICE;
+    rg_launch_ctx *cx = nullptr;
+    rg_status r = rg_launch_tiles(s, width, height, tiling, rgba_dev, rgb_dev, st, nullptr, &cx, stats != nullptr);
+    if (r != RG_OK || !stats) return r;
     unsigned long long c[4];
     if (!ok(hipMemcpyAsync(c, cx->counters, sizeof c, hipMemcpyDeviceToHost, st))) return RG_ERR_DEVICE;
     if (!ok(hipStreamSynchronize(st))) return RG_ERR_DEVICE;
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, cx->ev0, cx->ev1);
-    stats->rays.primary = c[0];
-    stats->rays.shadow = c[1];
-    stats->rays.secondary = c[2];
     stats->kernel_ms = ms;
-    stats->error_pixel = -1;
-    if (c[3] != 0) {
-        unsigned long long key = ~c[3];
-        stats->error_pixel = (int32_t)(key >> 8);
-        return (rg_status)(-(int32_t)(key & 0xff));
+    return rg_snap_status(c, stats);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- host-visible frames
+// The drop-in for rendering::render_image (rendering.rs:24-38) returns the
+// frame in HOST memory.  A 4K RGBA8 frame is 33 MB, about as long on PCIe
+// (~55 GB/s) as its render, so the frame is rendered in K row bands on two
+// render streams and band b's device-to-host copy (on a copy stream) runs
+// while bands b+1.. render.  A pinned caller buffer (hipHostMalloc'd, or
+// registered with rg_host_register) receives the DMA directly; a pageable
+// one is fed from a ring of pinned staging slots by host memcpy, overlapped
+// with the following bands' DMA.  Device framebuffer, staging, streams and
+// events belong to the scene and are reused across calls.
+namespace {
+
+int image_bands(const rg_scene *s, size_t px) {
+    if (s->image_bands > 0) return s->image_bands;
+    const size_t k = px / (2u << 20);  // ~2 Mpx per band
+    return (int)std::max<size_t>(1, std::min<size_t>(RG_IMAGE_STAGE_SLOTS + 1, k));
+}
+
+rg_status ensure_image_res(const rg_scene *s) {
+    rg_image_res &r = s->img;
+    if (r.cs) return RG_OK;
+    bool good = true;
+    for (hipStream_t &st : r.rs) good = good && ok(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    good = good && ok(hipStreamCreateWithFlags(&r.cs, hipStreamNonBlocking));
+    for (hipEvent_t &e : r.ev_done) good = good && ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t &e : r.ev_copy) good = good && ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    good = good && ok(hipEventCreate(&r.ev_t0)) && ok(hipEventCreate(&r.ev_t1)) &&
+           ok(hipEventCreateWithFlags(&r.ev_join, hipEventDisableTiming));
+    void *snap = nullptr;
+    good = good && ok(hipHostMalloc(&snap, RG_IMAGE_MAX_BANDS * 4 * sizeof(unsigned long long), hipHostMallocDefault));
+    r.h_snap = static_cast<unsigned long long *>(snap);
+    if (!good) {
+        release_image_res(r);
+        return RG_ERR_DEVICE;
     }
     return RG_OK;
 }
 
+template <class P>
+rg_status grow_device(P *&p, size_t &cap, size_t bytes) {
+    if (bytes <= cap) return RG_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    void *q = nullptr;
+    if (!ok(hipMalloc(&q, bytes))) { (void)hipGetLastError(); return RG_ERR_OUT_OF_MEMORY; }
+    p = static_cast<P *>(q);
+    cap = bytes;
+    return RG_OK;
+}
+
+}  // namespace
+
+rg_status rg_render_host(const rg_scene *s, uint32_t W, uint32_t H, const rg_tiling *t, uint8_t *rgba_out,
+                         float *rgb_out, rg_stats *stats) {
+    if (!s || !rgba_out || W == 0 || H == 0 || !tiling_valid(t)) return RG_ERR_INVALID_ARGUMENT;
+    if (W < H) return RG_ERR_PORTRAIT;
+    const uint32_t rows = rg_tiling_rows(H, t);
+    if ((unsigned long long)rows * W >= (1ull << 32) || (unsigned long long)H * W >= (1ull << 32))
+        return RG_ERR_INVALID_ARGUMENT;
+    if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
+    rg_status st = ensure_image_res(s);
+    if (st != RG_OK) return st;
+    rg_image_res &r = s->img;
+
+    // Bands.  A whole-frame tiling (stride 1) is re-cut into K bands of BR
+    // rows (tiling {BR, K, b} renders exactly rows [b BR, (b+1) BR)); a sharded
+    // tiling is rendered in one launch.
+    const bool banded = t->tile_stride == 1;
+    int K = 1;
+    uint32_t BR = rows;
+    if (banded) {
+        K = image_bands(s, (size_t)H * W);
+        BR = (H + (uint32_t)K - 1) / (uint32_t)K;
+        BR = (BR + 7u) & ~7u;  // whole 8x8 tiles per band
+        K = (int)((H + BR - 1) / BR);
+    }
+    const uint32_t dev_rows = banded ? (uint32_t)K * BR : rows;
+    const bool want_rgb = rgb_out != nullptr;
+    const size_t row4 = (size_t)W * 4, row12 = (size_t)W * 12;
+    if ((st = grow_device(r.d_rgba, r.d_rgba_cap, (size_t)dev_rows * row4 + 4)) != RG_OK) return st;
+    if (want_rgb && (st = grow_device(r.d_rgb, r.d_rgb_cap, (size_t)dev_rows * row12 + 4)) != RG_OK) return st;
+    const bool direct = rg_host_is_pinned(rgba_out, (size_t)rows * row4) &&
+                        (!want_rgb || rg_host_is_pinned(rgb_out, (size_t)rows * row12));
+    const int R = RG_IMAGE_STAGE_SLOTS;
+    const size_t slot_bytes = (size_t)BR * (row4 + (want_rgb ? row12 : 0));
+    if (!direct && (size_t)R * slot_bytes > r.h_stage_cap) {
+        if (r.h_stage) (void)hipHostFree(r.h_stage);
+        r.h_stage = nullptr;
+        r.h_stage_cap = 0;
+        if (!ok(hipHostMalloc(&r.h_stage, (size_t)R * slot_bytes, hipHostMallocDefault))) {
+            (void)hipGetLastError();
+            r.h_stage = nullptr;
+            return RG_ERR_OUT_OF_MEMORY;
+        }
+        r.h_stage_cap = (size_t)R * slot_bytes;
+    }
+    // host rows of band b: [b BR, min(H, (b+1) BR)) when banded, else all `rows`
+    auto host_rows = [&](int b) -> uint32_t {
+        if (!banded) return rows;
+        const uint32_t r0 = (uint32_t)b * BR;
+        return std::min(H, r0 + BR) - r0;
+    };
+    auto stage_rgba = [&](int b) { return static_cast<uint8_t *>(r.h_stage) + (size_t)(b % R) * slot_bytes; };
+    auto stage_rgb = [&](int b) { return reinterpret_cast<float *>(stage_rgba(b) + (size_t)BR * row4); };
+
+    if (!ok(hipEventRecord(r.ev_t0, r.rs[0])) || !ok(hipStreamWaitEvent(r.rs[1], r.ev_t0, 0))) return RG_ERR_DEVICE;
+    for (int b = 0; b < K; ++b) {
+        hipStream_t rs = r.rs[b & 1];
+        rg_tiling bt = banded ? rg_tiling{BR, (uint32_t)K, (uint32_t)b} : *t;
+        const size_t off = banded ? (size_t)b * BR : 0;
+        st = rg_launch_tiles(s, W, H, &bt, static_cast<uint8_t *>(r.d_rgba) + off * row4,
+                             want_rgb ? reinterpret_cast<float *>(static_cast<uint8_t *>(r.d_rgb) + off * row12) : nullptr,
+                             rs, r.h_snap + 4 * b, nullptr);
+        if (st != RG_OK) return st;
+        if (!ok(hipEventRecord(r.ev_done[b], rs))) return RG_ERR_DEVICE;
+    }
+    if (!ok(hipEventRecord(r.ev_join, r.rs[1])) || !ok(hipStreamWaitEvent(r.rs[0], r.ev_join, 0)) ||
+        !ok(hipEventRecord(r.ev_t1, r.rs[0])))
+        return RG_ERR_DEVICE;
+    auto enqueue_copy = [&](int b) -> bool {
+        const size_t off = banded ? (size_t)b * BR : 0;
+        const uint32_t n = host_rows(b);
+        uint8_t *dst4 = direct ? rgba_out + off * row4 : stage_rgba(b);
+        float *dst12 = want_rgb ? (direct ? rgb_out + off * (size_t)W * 3 : stage_rgb(b)) : nullptr;
+        if (!ok(hipStreamWaitEvent(r.cs, r.ev_done[b], 0))) return false;
+        if (n > 0 && !ok(hipMemcpyAsync(dst4, static_cast<uint8_t *>(r.d_rgba) + off * row4, (size_t)n * row4,
+                                        hipMemcpyDeviceToHost, r.cs)))
+            return false;
+        if (n > 0 && dst12 && !ok(hipMemcpyAsync(dst12, static_cast<uint8_t *>(r.d_rgb) + off * row12,
+                                                 (size_t)n * row12, hipMemcpyDeviceToHost, r.cs)))
+            return false;
+        return ok(hipEventRecord(r.ev_copy[b], r.cs));
+    };
+    if (direct) {
+        for (int b = 0; b < K; ++b)
+            if (!enqueue_copy(b)) return RG_ERR_DEVICE;
+        if (!ok(hipStreamSynchronize(r.cs))) return RG_ERR_DEVICE;
+    } else {
+        for (int b = 0; b < std::min(K, R); ++b)
+            if (!enqueue_copy(b)) return RG_ERR_DEVICE;
+        for (int b = 0; b < K; ++b) {
+            if (!ok(hipEventSynchronize(r.ev_copy[b]))) return RG_ERR_DEVICE;
+            const size_t off = banded ? (size_t)b * BR : 0;
+            const uint32_t n = host_rows(b);
+            std::memcpy(rgba_out + off * row4, stage_rgba(b), (size_t)n * row4);
+            if (want_rgb) std::memcpy(rgb_out + off * (size_t)W * 3, stage_rgb(b), (size_t)n * row12);
+            if (b + R < K && !enqueue_copy(b + R)) return RG_ERR_DEVICE;
+        }
+    }
+    if (!ok(hipStreamSynchronize(r.rs[0])) || !ok(hipStreamSynchronize(r.rs[1]))) return RG_ERR_DEVICE;
+    if (banded && rows > H) {  // padding rows of a whole-frame tiling whose tile_rows does not divide H
+        std::memset(rgba_out + (size_t)H * row4, 0, (size_t)(rows - H) * row4);
+        if (want_rgb) std::memset(rgb_out + (size_t)H * W * 3, 0, (size_t)(rows - H) * row12);
+    }
+    rg_stats total;
+    std::memset(&total, 0, sizeof total);
+    total.error_pixel = -1;
+    rg_status err = RG_OK;
+    for (int b = 0; b < K; ++b) {  // bands in row order: the first erroring band holds the lowest pixel
+        rg_stats bs;
+        const rg_status e = rg_snap_status(r.h_snap + 4 * b, &bs);
+        total.rays.primary += bs.rays.primary;
+        total.rays.shadow += bs.rays.shadow;
+        total.rays.secondary += bs.rays.secondary;
+        if (e != RG_OK && err == RG_OK) {
+            err = e;
+            total.error_pixel = bs.error_pixel;
+        }
+    }
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, r.ev_t0, r.ev_t1);
+    total.kernel_ms = ms;
+    if (stats) *stats = total;
+    return err;
+}
+
+extern "C" {
+
 rg_status rg_render_tiles(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
                           uint8_t *rgba_out, float *rgb_out, rg_stats *stats) {
-    if (!s || !rgba_out || width == 0 || height == 0 || !tiling_valid(tiling)) return RG_ERR_INVALID_ARGUMENT;
-    if (width < height) return RG_ERR_PORTRAIT;
-    if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
-    uint32_t rows = rg_tiling_rows(height, tiling);
-    size_t npx = (size_t)rows * width;
-    void *d_rgba = nullptr, *d_rgb = nullptr;
-    if (!ok(hipMalloc(&d_rgba, npx * 4 + 4))) return RG_ERR_OUT_OF_MEMORY;
-    if (rgb_out && !ok(hipMalloc(&d_rgb, npx * 12 + 4))) { (void)hipFree(d_rgba); return RG_ERR_OUT_OF_MEMORY; }
-    rg_stats local;
-    rg_stats *sp = stats ? stats : &local;
-    rg_status st = rg_render_tiles_async(s, width, height, tiling, (uint8_t *)d_rgba, (float *)d_rgb, nullptr, sp);
-    if (st == RG_OK || st < RG_ERR_INVALID_ARGUMENT) {
-        if (!ok(hipMemcpy(rgba_out, d_rgba, npx * 4, hipMemcpyDeviceToHost))) st = RG_ERR_DEVICE;
-        if (rgb_out && !ok(hipMemcpy(rgb_out, d_rgb, npx * 12, hipMemcpyDeviceToHost))) st = RG_ERR_DEVICE;
-    }
-    (void)hipFree(d_rgba);
-    if (d_rgb) (void)hipFree(d_rgb);
-    return st;
+    return rg_render_host(s, width, height, tiling, rgba_out, rgb_out, stats);
 }
 
 rg_status rg_render_image(const rg_scene *s, uint32_t width, uint32_t height, uint8_t *rgba_out, rg_stats *stats) {
     rg_tiling whole = {height ? height : 1, 1, 0};
-    return rg_render_tiles(s, width, height, &whole, rgba_out, nullptr, stats);
+    return rg_render_host(s, width, height, &whole, rgba_out, nullptr, stats);
 }
 
+rg_status rg_host_register(void *ptr, size_t bytes) {
+    if (!ptr || bytes == 0) return RG_ERR_INVALID_ARGUMENT;
+    if (!ok(hipHostRegister(ptr, bytes, hipHostRegisterDefault))) {
+        (void)hipGetLastError();
+        return RG_ERR_DEVICE;
+    }
+    return RG_OK;
+}
+
+rg_status rg_host_unregister(void *ptr) {
+    if (!ptr) return RG_ERR_INVALID_ARGUMENT;
+    if (!ok(hipHostUnregister(ptr))) {
+        (void)hipGetLastError();
+        return RG_ERR_DEVICE;
+    }
+    return RG_OK;
+}
+
+// Tile-completion streaming.  Bands of `tile_rows` rows render on the scene's
+// render stream into two device slots; each band's copy to one of two pinned
+// host slots runs on the copy stream once it is rendered.  While the
+// callback holds band b, bands b+1 and b+2 render and band b+1 is copied:
+// band b+2 reuses band b's device slot (its copy is done: the host waited for
+// it) and its copy waits for band b's callback to return (host order).
 rg_status rg_render_stream(const rg_scene *s, uint32_t width, uint32_t height, uint32_t tile_rows,
                            rg_tile_callback on_tile, void *user, rg_stats *stats) {
     if (!s || !on_tile || width == 0 || height == 0 || tile_rows == 0) return RG_ERR_INVALID_ARGUMENT;
     if (width < height) return RG_ERR_PORTRAIT;
     if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
-    // Bands are rendered one after another on one stream; while the host hands
-    // band b to the callback, band b+1 is already rendering (double-buffered
-    // pinned staging).  Counters accumulate on the host.
-    uint32_t nb = (height + tile_rows - 1) / tile_rows;
-    size_t band_px = (size_t)tile_rows * width;
-    void *d_buf[2] = {nullptr, nullptr};
-    void *h_buf[2] = {nullptr, nullptr};
-    hipStream_t stream = nullptr;
-    hipEvent_t done[2] = {nullptr, nullptr};
-    rg_status st = RG_OK;
+    rg_status st = ensure_image_res(s);
+    if (st != RG_OK) return st;
+    rg_image_res &r = s->img;
+    const uint32_t nb = (height + tile_rows - 1) / tile_rows;
+    const size_t band_bytes = (size_t)tile_rows * width * 4;
+    if ((st = grow_device(r.d_rgba, r.d_rgba_cap, 2 * band_bytes + 4)) != RG_OK) return st;
+    if (2 * band_bytes > r.h_stage_cap) {
+        if (r.h_stage) (void)hipHostFree(r.h_stage);
+        r.h_stage = nullptr;
+        r.h_stage_cap = 0;
+        if (!ok(hipHostMalloc(&r.h_stage, 2 * band_bytes, hipHostMallocDefault))) {
+            (void)hipGetLastError();
+            r.h_stage = nullptr;
+            return RG_ERR_OUT_OF_MEMORY;
+        }
+        r.h_stage_cap = 2 * band_bytes;
+    }
+    uint8_t *dslot[2] = {static_cast<uint8_t *>(r.d_rgba), static_cast<uint8_t *>(r.d_rgba) + band_bytes};
+    uint8_t *hslot[2] = {static_cast<uint8_t *>(r.h_stage), static_cast<uint8_t *>(r.h_stage) + band_bytes};
+    const int E = RG_IMAGE_MAX_BANDS;  // event / snapshot ring
+    auto rows_of = [&](uint32_t b) { return (b + 1) * tile_rows <= height ? tile_rows : height - b * tile_rows; };
+    auto render = [&](uint32_t b) -> rg_status {
+        rg_tiling tb = {tile_rows, nb, b};
+        hipStream_t rs = r.rs[b & 1];
+        rg_status e = rg_launch_tiles(s, width, height, &tb, dslot[b & 1], nullptr, rs, r.h_snap + 4 * (b % E), nullptr);
+        if (e == RG_OK && !ok(hipEventRecord(r.ev_done[b % E], rs))) e = RG_ERR_DEVICE;
+        return e;
+    };
+    auto copy = [&](uint32_t b) -> rg_status {
+        if (!ok(hipStreamWaitEvent(r.cs, r.ev_done[b % E], 0)) ||
+            !ok(hipMemcpyAsync(hslot[b & 1], dslot[b & 1], (size_t)rows_of(b) * width * 4, hipMemcpyDeviceToHost, r.cs)) ||
+            !ok(hipEventRecord(r.ev_copy[b % E], r.cs)))
+            return RG_ERR_DEVICE;
+        return RG_OK;
+    };
     rg_ray_counts total = {0, 0, 0};
-    float total_ms = 0.0f;
     int32_t err_pixel = -1;
     rg_status err_status = RG_OK;
-    for (int i = 0; i < 2 && st == RG_OK; ++i) {
-        if (!ok(hipMalloc(&d_buf[i], band_px * 4 + 4)) || !ok(hipHostMalloc(&h_buf[i], band_px * 4 + 4)))
-            st = RG_ERR_OUT_OF_MEMORY;
-        else if (!ok(hipEventCreate(&done[i])))
-            st = RG_ERR_DEVICE;
+    if (!ok(hipEventRecord(r.ev_t0, r.rs[0])) || !ok(hipStreamWaitEvent(r.rs[1], r.ev_t0, 0))) st = RG_ERR_DEVICE;
+    for (uint32_t b = 0; st == RG_OK && b < std::min<uint32_t>(nb, 2); ++b) {
+        st = render(b);
+        if (st == RG_OK) st = copy(b);
     }
-    if (st == RG_OK && !ok(hipStreamCreate(&stream))) st = RG_ERR_DEVICE;
     for (uint32_t b = 0; st == RG_OK && b < nb; ++b) {
-        int k = b & 1;
-        rg_tiling t = {tile_rows, nb, b};
+        if (!ok(hipEventSynchronize(r.ev_copy[b % E]))) { st = RG_ERR_DEVICE; break; }
         rg_stats bs;
-        st = rg_render_tiles_async(s, width, height, &t, (uint8_t *)d_buf[k], nullptr, stream, &bs);
-        if (st < RG_ERR_INVALID_ARGUMENT && st != RG_ERR_DEVICE && st != RG_ERR_OUT_OF_MEMORY) {
-            if (err_status == RG_OK) { err_status = st; err_pixel = bs.error_pixel; }
-            st = RG_OK;
-        }
-        if (st != RG_OK) break;
+        const rg_status e = rg_snap_status(r.h_snap + 4 * (b % E), &bs);
         total.primary += bs.rays.primary;
         total.shadow += bs.rays.shadow;
         total.secondary += bs.rays.secondary;
-        total_ms += bs.kernel_ms;
-        uint32_t rows = (b + 1) * tile_rows <= height ? tile_rows : height - b * tile_rows;
-        if (!ok(hipMemcpyAsync(h_buf[k], d_buf[k], (size_t)rows * width * 4, hipMemcpyDeviceToHost, stream)) ||
-            !ok(hipStreamSynchronize(stream))) {
-            st = RG_ERR_DEVICE;
-            break;
-        }
-        if (on_tile(b * tile_rows, rows, width, (const uint8_t *)h_buf[k], user) != 0) {
+        if (e != RG_OK && err_status == RG_OK) { err_status = e; err_pixel = bs.error_pixel; }
+        if (b + 2 < nb && (st = render(b + 2)) != RG_OK) break;  // into band b's device slot (copied)
+        if (on_tile(b * tile_rows, rows_of(b), width, hslot[b & 1], user) != 0) {
             st = RG_ERR_CANCELLED;
             break;
         }
+        if (b + 2 < nb) st = copy(b + 2);  // into band b's host slot, released by the callback
     }
-    if (stream) (void)hipStreamDestroy(stream);
-    for (int i = 0; i < 2; ++i) {
-        if (d_buf[i]) (void)hipFree(d_buf[i]);
-        if (h_buf[i]) (void)hipHostFree(h_buf[i]);
-        if (done[i]) (void)hipEventDestroy(done[i]);
-    }
+    (void)hipEventRecord(r.ev_join, r.rs[1]);
+    (void)hipStreamWaitEvent(r.rs[0], r.ev_join, 0);
+    (void)hipEventRecord(r.ev_t1, r.rs[0]);
+    (void)hipStreamSynchronize(r.rs[0]);
+    (void)hipStreamSynchronize(r.rs[1]);
+    (void)hipStreamSynchronize(r.cs);
     if (stats) {
+        float ms = 0.0f;
+        (void)hipEventElapsedTime(&ms, r.ev_t0, r.ev_t1);
         stats->rays = total;
-        stats->kernel_ms = total_ms;
+        stats->kernel_ms = ms;
         stats->error_pixel = err_pixel;
     }
     if (st == RG_OK && err_status != RG_OK) return err_status;
@@ -642,6 +1001,12 @@ rg_status rg_debug_set_tile_order(rg_scene *s, int32_t mode) {
     return RG_OK;
 }
 
+rg_status rg_debug_set_image_bands(rg_scene *s, int32_t bands) {
+    if (!s || bands < 0 || bands > RG_IMAGE_MAX_BANDS) return RG_ERR_INVALID_ARGUMENT;
+    s->image_bands = bands;
+    return RG_OK;
+}
+
 rg_status rg_debug_counters(const rg_scene *s, uint64_t out[16]) {
     if (!s || !out) return RG_ERR_INVALID_ARGUMENT;
     if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
@@ -662,7 +1027,7 @@ rg_status rg_trace(const rg_scene *s, const double *rays, uint32_t n, double *di
         st = RG_ERR_OUT_OF_MEMORY;
     rg_launch_ctx *cx = ctx_for(s, nullptr);
     if (!cx) st = RG_ERR_OUT_OF_MEMORY;
-    RgKernelArgs a = make_args(s);
+    RgKernelArgs a = rg_make_args(s);
     unsigned long long c[4] = {0, 0, 0, 0};
     if (st == RG_OK) { s->last = cx; a.counters = cx->counters; }
     if (st == RG_OK && (!ok(hipMemcpy(d_rays, rays, (size_t)n * 48, hipMemcpyHostToDevice)) ||
@@ -675,7 +1040,7 @@ rg_status rg_trace(const rg_scene *s, const double *rays, uint32_t n, double *di
     if (d_rays) (void)hipFree(d_rays);
     if (d_dist) (void)hipFree(d_dist);
     if (d_body) (void)hipFree(d_body);
-    if (st == RG_OK && c[3] != 0) st = (rg_status)(-(int32_t)((~c[3]) & 0xff));
+    if (st == RG_OK && c[3] != 0) st = decode_error(c[3], nullptr);
     return st;
 }
 

@@ -142,7 +142,15 @@ struct RgKernelArgs {
     float *rgb;              // nullable, out_rows * width * 3
     const uint32_t *tile_perm;     // nullable: dequeue order of the 8x8 tiles (expensive first)
     unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=~error key [16+16q]=tile queue heads (RG_COUNTER_WORDS words)
+    // frames of the shading tree for depths above the compiled arrays (rg_kernels.hip FrameStack<0>)
+    void *deep_stack;        // grid threads x (max_depth - 1) frames, frame i of thread g at [i * deep_stride + g]
+    uint32_t deep_stride;    // threads of the grid the buffer was sized for
+    int32_t nan_scene;       // a body or light parameter is non-finite or >= 1e100: NaN distances possible
+    unsigned long long *err_sticky;  // nullable: the launch context's error word that survives launches
 };
+
+// sizeof(Frame) in rg_kernels.hip (the deep frame buffer is sized on the host)
+#define RG_FRAME_BYTES 88
 
 #ifndef RG_LB
 #define RG_LB 3                   // lights per shadow batch on the light path (its LB template parameter)

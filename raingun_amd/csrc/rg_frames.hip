@@ -36,6 +36,14 @@ __global__ __launch_bounds__(256) void rg_reinterleave_kernel(const uint32_t *ga
 
 }  // namespace
 
+hipError_t rg_launch_reinterleave(const void *gathered, void *image, uint32_t width, uint32_t height, uint32_t tile_rows,
+                                  uint32_t world, uint32_t slot_rows, hipStream_t stream) {
+    dim3 grid((width + 255u) / 256u, height);
+    hipLaunchKernelGGL(rg_reinterleave_kernel, grid, dim3(256), 0, stream, static_cast<const uint32_t *>(gathered),
+                       static_cast<uint32_t *>(image), width, height, tile_rows, world, slot_rows);
+    return hipGetLastError();
+}
+
 struct rg_frames {
     const rg_scene *scene = nullptr;
     int device = 0;
@@ -51,6 +59,8 @@ struct rg_frames {
     std::vector<hipEvent_t> rendered, sent, done;
     unsigned long long k = 0;
     int last = -1;
+    rg_status err = RG_OK;     // first device error of any frame (sticky until destroy)
+    int32_t err_pixel = -1;
 };
 
 namespace {
@@ -67,7 +77,10 @@ void frames_release(rg_frames *f) {
     for (hipEvent_t e : f->rendered) (void)hipEventDestroy(e);
     for (hipEvent_t e : f->sent) (void)hipEventDestroy(e);
     for (hipEvent_t e : f->done) (void)hipEventDestroy(e);
-    for (hipStream_t s : f->render) (void)hipStreamDestroy(s);
+    for (hipStream_t s : f->render) {
+        (void)rg_scene_release_stream(const_cast<rg_scene *>(f->scene), s);  // its launch state goes with it
+        (void)hipStreamDestroy(s);
+    }
     if (f->comm_stream) (void)hipStreamDestroy(f->comm_stream);
     if (f->side) (void)hipStreamDestroy(f->side);
     delete f;
@@ -157,11 +170,10 @@ rg_status rg_frames_step(rg_frames *f) {
     if (!ok(hipEventRecord(f->sent[b], f->comm_stream))) return RG_ERR_DEVICE;
     if (f->rank == 0) {
         if (!ok(hipStreamWaitEvent(f->side, f->sent[b], 0))) return RG_ERR_DEVICE;
-        dim3 grid((f->w + 255u) / 256u, f->h);
-        hipLaunchKernelGGL(rg_reinterleave_kernel, grid, dim3(256), 0, f->side,
-                           static_cast<const uint32_t *>(f->gathered[b]), static_cast<uint32_t *>(f->image[b]), f->w,
-                           f->h, f->T, (uint32_t)f->world, f->slot_rows);
-        if (!ok(hipGetLastError()) || !ok(hipEventRecord(f->done[b], f->side))) return RG_ERR_DEVICE;
+        if (!ok(rg_launch_reinterleave(f->gathered[b], f->image[b], f->w, f->h, f->T, (uint32_t)f->world, f->slot_rows,
+                                       f->side)) ||
+            !ok(hipEventRecord(f->done[b], f->side)))
+            return RG_ERR_DEVICE;
     } else if (!ok(hipEventRecord(f->done[b], f->comm_stream))) {
         return RG_ERR_DEVICE;
     }
@@ -172,10 +184,26 @@ rg_status rg_frames_step(rg_frames *f) {
 
 rg_status rg_frames_flush(rg_frames *f) {
     if (!f) return RG_ERR_INVALID_ARGUMENT;
-    for (hipStream_t s : f->render)
+    for (hipStream_t s : f->render) {
         if (!ok(hipStreamSynchronize(s))) return RG_ERR_DEVICE;
+        // device errors of this rank's renders (the reference panics: rendering.rs, bodies.rs:324, scene.rs:38)
+        int32_t px = -1;
+        const rg_status e = rg_stream_status(f->scene, s, &px);
+        if (e == RG_ERR_DEVICE) return e;
+        if (e != RG_OK && (f->err == RG_OK || px < f->err_pixel)) {
+            f->err = e;
+            f->err_pixel = px;
+        }
+    }
     if (!ok(hipStreamSynchronize(f->comm_stream)) || !ok(hipStreamSynchronize(f->side))) return RG_ERR_DEVICE;
-    return RG_OK;
+    return f->err;
+}
+
+rg_status rg_frames_status(rg_frames *f, int32_t *error_pixel) {
+    if (!f) return RG_ERR_INVALID_ARGUMENT;
+    const rg_status st = rg_frames_flush(f);
+    if (error_pixel) *error_pixel = f->err_pixel;
+    return st;
 }
 
 const uint8_t *rg_frames_image(const rg_frames *f) {
@@ -185,10 +213,11 @@ const uint8_t *rg_frames_image(const rg_frames *f) {
 
 rg_status rg_frames_read_image(const rg_frames *f, uint8_t *host_out) {
     if (!f || !host_out || f->rank != 0 || f->last < 0) return RG_ERR_INVALID_ARGUMENT;
-    if (rg_frames_flush(const_cast<rg_frames *>(f)) != RG_OK) return RG_ERR_DEVICE;
+    const rg_status st = rg_frames_flush(const_cast<rg_frames *>(f));
+    if (st == RG_ERR_DEVICE) return st;
     if (!ok(hipMemcpy(host_out, f->image[f->last], (size_t)f->h * f->w * 4, hipMemcpyDeviceToHost)))
         return RG_ERR_DEVICE;
-    return RG_OK;
+    return st;  // the frame is delivered; a device error any frame raised is reported
 }
 
 }  // extern "C"

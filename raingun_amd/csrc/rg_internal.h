@@ -1,0 +1,137 @@
+// rg_internal.h — host-side state behind the opaque rg_scene handle, shared
+// by rg_capi.hip (scene upload, launches, host-visible frames, streaming),
+// rg_frames.hip (frames in flight over N processes) and rg_multi.hip (one
+// process driving N devices).  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <vector>
+
+#include "../../include/raingun.h"
+#include "../../include/raingun_debug.h"
+#include "rg_device.h"
+
+// Per-stream launch state (ray counters, tile-queue heads, error words, tile
+// ordering scratch, deep frame buffer, timing events).  Launches on distinct
+// streams may run concurrently (frames in flight), so they must not share it;
+// launches on one stream are ordered by the stream and reuse it.
+struct rg_launch_ctx {
+    hipStream_t stream = nullptr;
+    unsigned long long *counters = nullptr;  // RG_COUNTER_WORDS words (rg_device.h), reset by every launch
+    unsigned long long *sticky = nullptr;    // first error of any launch since rg_stream_status cleared it
+    uint32_t *tile_cost = nullptr, *tile_perm = nullptr;  // probe/sort scratch (rg_launch_tile_order), order
+    size_t tile_cap = 0;
+    void *deep = nullptr;  // frames for depths above the compiled arrays (rg_kernels.hip FrameStack<0>)
+    size_t deep_bytes = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+#define RG_IMAGE_STAGE_SLOTS 3  // pinned staging slots of the host-visible image path
+#define RG_IMAGE_MAX_BANDS 16   // events / counter snapshots per host-visible render or stream ring
+
+// Resources of the host-visible paths (rg_render_image / rg_render_tiles /
+// rg_render_stream), owned by the scene and reused across calls.
+struct rg_image_res {
+    hipStream_t rs[2] = {nullptr, nullptr};  // render streams (bands alternate)
+    hipStream_t cs = nullptr;                // device-to-host copies
+    hipEvent_t ev_done[RG_IMAGE_MAX_BANDS] = {};
+    hipEvent_t ev_copy[RG_IMAGE_MAX_BANDS] = {};
+    hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_join = nullptr;
+    void *d_rgba = nullptr;
+    size_t d_rgba_cap = 0;
+    void *d_rgb = nullptr;
+    size_t d_rgb_cap = 0;
+    void *h_stage = nullptr;  // pinned
+    size_t h_stage_cap = 0;
+    unsigned long long *h_snap = nullptr;  // pinned: 4 counter words per band
+};
+
+// Everything rg_scene_create uploads, as host tables (kept for replicas on
+// other devices: rg_render_multi).
+struct rg_host_tables {
+    std::vector<RgSph> sph;
+    std::vector<RgSphF> sphf;
+    std::vector<RgSphF2> sphf2;
+    std::vector<double> sph_cc;
+    std::vector<int32_t> sph_id, pln_id, dsk_id, box_id;
+    std::vector<RgPln> pln;
+    std::vector<RgDsk> dsk;
+    std::vector<RgBox> box;
+    std::vector<RgBodyDev> bodies;
+    std::vector<RgMatDev> mats;
+    std::vector<RgLightDev> lights;
+    std::vector<RgBvhNode> nodes;
+    std::vector<uint32_t> tex_w, tex_h;
+    std::vector<std::vector<uint32_t>> texels;
+};
+
+struct rg_multi_res;  // rg_multi.hip
+
+struct rg_scene {
+    int device = 0;
+    double fov = 90.0;
+    float def[3] = {0, 0, 0};
+    uint32_t max_depth = 10;
+    int32_t n_sph = 0, n_pln = 0, n_dsk = 0, n_box = 0, n_bodies = 0, n_lights = 0, n_textures = 0;
+    bool nan_scene = false;  // NaN distances possible (rg_kernels.hip ray_exotic)
+    std::vector<void *> allocations;
+    RgSph *sph = nullptr;
+    double *sph_cc = nullptr;
+    RgSphF *sphf = nullptr;
+    RgSphF2 *sphf2 = nullptr;
+    int32_t path = RG_PATH_AUTO;
+    int32_t *sph_id = nullptr, *pln_id = nullptr, *dsk_id = nullptr, *box_id = nullptr;
+    RgPln *pln = nullptr;
+    RgDsk *dsk = nullptr;
+    RgBox *box = nullptr;
+    RgBodyDev *bodies = nullptr;
+    RgMatDev *mats = nullptr;
+    RgLightDev *lights = nullptr;
+    RgTexDev *texs = nullptr;
+    RgBvhNode *nodes = nullptr;  // sphere BVH (sphere tables are in its leaf order)
+    int32_t n_nodes = 0;
+    int32_t lane_stack = 0;      // per-lane walk stack entries the tree needs (0: per-lane walk unavailable)
+    int32_t lane_min_depth = 1;  // rays of this depth and deeper walk the BVH per lane
+    bool bvh_enabled = true;
+    float bvh_obound = 0.0f;
+    double bvh_rbound = 0.0, bvh_margin = 0.0, bvh_extent = 0.0;
+    rg_bvh_info bvh_info{};
+    int tile_order = -1;  // expensive tiles first (rg_kernels.hip "tile ordering"): -1 auto (heavy path), 0, 1
+    int image_bands = 0;  // host-visible frames: row bands per render (0: by frame size, rg_capi.hip image_bands)
+    std::shared_ptr<const rg_host_tables> host;
+    mutable std::vector<rg_launch_ctx *> ctxs;  // one per stream used
+    mutable rg_launch_ctx *last = nullptr;       // the context of the latest launch (rg_debug_counters)
+    mutable rg_image_res img;
+    mutable rg_multi_res *multi = nullptr;
+};
+
+// Kernel arguments of a scene (tables, LDS arena, frame constants).
+RgKernelArgs rg_make_args(const rg_scene *s);
+
+// Enqueue one tiled render on `stream` (the body of rg_render_tiles_async).
+// snap (nullable, host memory, pinned for a truly asynchronous copy): the
+// launch's 4 counter words (rays by class, error key) are copied there after
+// the kernel.  ctx_out (nullable): the stream's launch context.  timed: record
+// the context's ev0/ev1 around the launch (kernel_ms).
+rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
+                          uint8_t *rgba_dev, float *rgb_dev, hipStream_t stream, unsigned long long *snap,
+                          rg_launch_ctx **ctx_out, bool timed = false);
+
+// Ray counts and status of a counter snapshot (stats nullable).
+rg_status rg_snap_status(const unsigned long long *snap, rg_stats *stats);
+
+// Host-visible render of `tiling` into host buffers (rg_render_tiles / rg_render_image).
+rg_status rg_render_host(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
+                         uint8_t *rgba_out, float *rgb_out, rg_stats *stats);
+
+// Is [p, p + bytes) page-locked host memory the DMA engine can write directly?
+bool rg_host_is_pinned(const void *p, size_t bytes);
+
+// A copy of `src` on `device` (same tables, same settings).
+rg_status rg_scene_replica(const rg_scene *src, int32_t device, rg_scene **out);
+void rg_scene_free(rg_scene *s);
+void rg_sync_settings(rg_scene *dst, const rg_scene *src);  // depth, path, BVH, lane depth, tile order
+
+// rg_multi.hip: free the scene's multi-GPU resources (replicas, communicators).
+void rg_multi_release(const rg_scene *s);

@@ -18,7 +18,10 @@
 // Division and sqrt are the correctly-rounded hipcc expansions.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "../../include/raingun.h"
 #include "rg_bvh_ray.h"
@@ -76,6 +79,7 @@ __device__ __forceinline__ void raise_error(const RgKernelArgs &a, uint32_t pixe
     // lowest pixel wins: max of the complemented key; 0 (memset) = no error
     unsigned long long key = ((unsigned long long)pixel << 8) | (unsigned long long)(-status);
     atomicMax(&a.counters[3], ~key);
+    if (a.err_sticky) atomicMax(a.err_sticky, ~key);  // survives the next launch's counter reset
 }
 
 // ---------------------------------------------------------------- closest hit
@@ -800,6 +804,19 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
     }
 }
 
+// A query ray whose arithmetic may overflow.  With every scene coordinate
+// below 1e100 in magnitude (the host's `nan_scene` test, rg_capi.hip), a ray
+// with |o_k| < 1e100 and |d_k| < 1e50 keeps every intermediate of the body
+// tests (bodies.rs:92-119, 136-148, 173-192, 242-282) finite, so no hit
+// distance can be NaN and Scene::trace's `partial_cmp().unwrap()`
+// (scene.rs:38) cannot panic.  Anything else (NaN/inf included: the
+// comparisons are false) is exotic and takes the exact, fully counted query.
+__device__ __forceinline__ bool ray_exotic(V3 o, V3 d) {
+    const bool ok = fabs(o.x) < 1e100 && fabs(o.y) < 1e100 && fabs(o.z) < 1e100 && fabs(d.x) < 1e50 &&
+                    fabs(d.y) < 1e50 && fabs(d.z) < 1e50;
+    return !ok;
+}
+
 // ---------------------------------------------------------------- shadow batches
 // shade_diffuse traces one shadow ray per light from the SAME origin
 // hit + n*bias (rendering.rs:141-150).  A lane traces up to RG_LB of them in
@@ -1062,6 +1079,33 @@ struct Frame {
     int cdepth;   // depth of this node's children
 };
 
+// The lane's stack of open frames: at most max_recursion_depth - 1 deep
+// (rendering.rs:122-130 stops at depth >= max).  MAXD > 0: a per-lane array
+// (scratch).  MAXD == 0 (depths above the largest compiled array,
+// scene.rs:16 is a u32): frames live in a global buffer owned by the launch
+// context, frame i of the grid's thread g at base[i * stride + g], so frame
+// i of a wave is one contiguous run; that launch is persistent, so the grid
+// (and the buffer) stays bounded whatever the frame size.
+static_assert(sizeof(Frame) == RG_FRAME_BYTES, "host sizes the deep frame buffer with RG_FRAME_BYTES");
+
+template <int MAXD>
+struct FrameStack {
+    Frame f[MAXD];
+    __device__ __forceinline__ void init(const RgKernelArgs &) {}
+    __device__ __forceinline__ Frame &operator[](int i) { return f[i]; }
+};
+template <>
+struct FrameStack<0> {
+    Frame *base;
+    uint32_t stride;
+    __device__ __forceinline__ void init(const RgKernelArgs &a) {
+        stride = a.deep_stride;
+        base = static_cast<Frame *>(a.deep_stack) + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    }
+    __device__ __forceinline__ Frame &operator[](int i) { return base[(size_t)i * stride]; }
+};
+
+
 __device__ __forceinline__ uint32_t out_row_to_y(const RgKernelArgs &a, uint32_t orow) {
     uint32_t tl = orow / a.tile_rows, r = orow - tl * a.tile_rows;
     unsigned long long y = ((unsigned long long)tl * a.tile_stride + a.tile_offset) * a.tile_rows + r;
@@ -1309,7 +1353,8 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     const C3 def = c3(a.def[0], a.def[1], a.def[2]);
     const int max_depth = (int)a.max_depth;
     uint32_t n_prim = 0, n_shadow = 0, n_sec = 0;
-    Frame stk[MAXD];
+    FrameStack<MAXD> stk;
+    stk.init(a);
 
     // Sharded tile queue: RG_NQ heads, each owning a contiguous band of tiles
     // (one 128-B line per head).  A single head saturates at ~88 dequeues/us
@@ -1704,7 +1749,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             if (tile == 0xFFFFFFFFu) {
                 tiles_left = false;
             } else {
-                constexpr uint32_t kmax = LB > 1 ? RG_LIGHT_TILES_PER_WAVE : RG_HEAVY_TILES_PER_WAVE;
+                constexpr uint32_t kmax = MAXD == 0 ? 0u : LB > 1 ? RG_LIGHT_TILES_PER_WAVE : RG_HEAVY_TILES_PER_WAVE;
                 if constexpr (kmax > 0) {
                     // non-persistent: a wave renders at most kmax tiles, so the grid
                     // drains through the hardware dispatcher wave (block) by wave
@@ -1764,6 +1809,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                     const int w = __builtin_amdgcn_readlane(want, o);
                     const int oli = __builtin_amdgcn_readlane(li, o);
                     const int ohd = __builtin_amdgcn_readlane(hdepth, o);
+                    const uint32_t opix = (uint32_t)__builtin_amdgcn_readlane((int)pixel, o);
                     const V3 ohp = v3(readlane_d(hp.x, o), readlane_d(hp.y, o), readlane_d(hp.z, o));
                     const V3 oso = v3(readlane_d(q.o.x, o), readlane_d(q.o.y, o), readlane_d(q.o.z, o));
                     uint32_t packed = 0u;
@@ -1776,6 +1822,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                             hp = ohp;
                             q.o = oso;  // hit + n * bias (rendering.rs:148)
                             hdepth = ohd;
+                            pixel = opix;  // error reports name the owner's pixel
                             light_dir_dist(T.lights[oli + 1 + k], hp, sb.d[0], sb.ld[0]);
                             mode = MODE_SHADOW_H;
                         }
@@ -1850,19 +1897,54 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                 const bool shadow = mode == MODE_SHADOW || mode == MODE_SHADOW_H;
                 r1.d = shadow ? sb.d[0] : q.d;
                 const bool lane_walk = (shadow ? hdepth : qdepth) >= (int)a.lane_min_depth;
-                trace_query<F32F, BVH>(a, src, r1, shadow, sb.ld[0], c, o1, lane_walk);
+                // a shadow ray that could see a NaN distance (ray_exotic) runs as a
+                // fully counted closest-hit query: in_light = none || dist > light
+                // distance (rendering.rs:150-155), the scene.rs:38 panic iff >= 2 hits, one NaN
+                const bool exact = shadow && (a.nan_scene || ray_exotic(r1.o, r1.d));
+                trace_query<F32F, BVH>(a, src, r1, shadow && !exact, sb.ld[0], c, o1, lane_walk);
+                if (exact) {
+                    o1 = c.id >= 0 && !(c.t > sb.ld[0]);
+                    if (c.nan && c.nhit >= 2) raise_error(a, pixel, RG_ERR_NAN_DISTANCE);
+                }
                 occl = o1 ? 1u : 0u;
             }
         } else {
             // closest-hit lanes and shadow-batch lanes walk the body tables in two
-            // passes; each pass is skipped when no lane of the wave needs it
-            if (mode == MODE_CLOSEST) {
-#ifndef RG_DBG_NO_SEC_TRACE
-                bool unused = false;
-                trace_query<F32F, BVH>(a, src, q, false, 0.0, c, unused);
-#endif
-            }
+            // passes; each pass is skipped when no lane of the wave needs it.  A
+            // batch that could see a NaN distance (ray_exotic) instead runs its
+            // lights one by one through the closest-hit pass, fully counted
+            // (rendering.rs:150-155; the scene.rs:38 panic iff >= 2 hits, one NaN).
+            bool exact = false;
             if (mode == MODE_SHADOW) {
+                exact = a.nan_scene != 0;
+#pragma unroll
+                for (int l = 0; l < LB; ++l) exact |= ((occl_full >> l) & 1u) && ray_exotic(q.o, sb.d[l]);
+            }
+            const int passes = mode == MODE_CLOSEST ? 1 : exact ? LB : 0;
+            if (exact) occl = ~occl_full & ((1u << LB) - 1u);
+            for (int l = 0; __any(l < passes); ++l) {
+                if (l < passes && (mode == MODE_CLOSEST || ((occl_full >> l) & 1u))) {
+                    Ray rq;
+                    rq.o = q.o;
+                    rq.d = q.d;
+                    double ld = 0.0;
+                    if (exact) {
+#pragma unroll
+                        for (int k = 0; k < LB; ++k)
+                            if (k == l) { rq.d = sb.d[k]; ld = sb.ld[k]; }
+                        closest_init(c);
+                    }
+#ifndef RG_DBG_NO_SEC_TRACE
+                    bool unused = false;
+                    trace_query<F32F, BVH>(a, src, rq, false, 0.0, c, unused);
+#endif
+                    if (exact) {
+                        if (c.id >= 0 && !(c.t > ld)) occl |= 1u << l;
+                        if (c.nan && c.nhit >= 2) raise_error(a, pixel, RG_ERR_NAN_DISTANCE);
+                    }
+                }
+            }
+            if (mode == MODE_SHADOW && !exact) {
                 occl = ~occl_full & ((1u << LB) - 1u);  // absent slots count as done
 #ifndef RG_DBG_NO_SHADOW_TRACE
                 trace_shadow<LB>(a, src, q.o, sb, (1u << LB) - 1u, occl);
@@ -2084,8 +2166,46 @@ extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scra
 #ifndef RG_LIGHT_BLOCK_WAVES
 #define RG_LIGHT_BLOCK_WAVES 1  // light path: waves per block (blocks retire wave by wave)
 #endif
+#ifndef RG_DEEP_BLOCKS_PER_CU
+#define RG_DEEP_BLOCKS_PER_CU 8  // deep-stack light launches: resident one-wave blocks per CU (bounds the frame buffer)
+#endif
+
+// Occupancy of one kernel instantiation on the CURRENT device, cached per
+// (device, kernel, dynamic LDS): hipFuncSetAttribute and the occupancy query
+// are per device, and scenes on different devices (rg_render_multi) or host
+// threads may launch the same instantiation.
+struct OccKey {
+    int dev;
+    const void *kern;
+    size_t lds;
+};
+static std::mutex occ_mu;
+static std::vector<std::pair<OccKey, std::pair<int, int>>> occ_cache;  // -> (CUs, blocks per CU)
+
+static hipError_t occupancy(const void *kern, int threads, size_t lds, int &cus, int &per_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> g(occ_mu);
+    for (const auto &e : occ_cache)
+        if (e.first.dev == dev && e.first.kern == kern && e.first.lds == lds) {
+            cus = e.second.first;
+            per_cu = e.second.second;
+            return hipSuccess;
+        }
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorInvalidValue;
+    if (lds > 64 * 1024 && hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return hipErrorInvalidValue;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess)
+        return hipErrorInvalidValue;
+    if (per_cu < 1) return hipErrorInvalidConfiguration;
+    occ_cache.push_back({OccKey{dev, kern, lds}, {cus, per_cu}});
+    return hipSuccess;
+}
+
+// Launch (or, with grid_threads != nullptr, only size: the threads of the
+// grid, which a MAXD == 0 launch needs for its frame buffer) one instantiation.
 template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
-static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream) {
+static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream, size_t *grid_threads) {
     // Block size.  The heavy path shares one LDS copy of the scene (and the
     // BVH stacks / task pool) among the CU's 4*WPS waves: one block per CU.
     // The light path's scene is a few KB, so it runs small blocks, each with
@@ -2094,32 +2214,26 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     // waves that finished (a 4*WPS-wave block would keep the CU until its
     // slowest wave -- one refractive tile -- is done).
     constexpr int threads = LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS;  // LB > 1: the light path
-    static int cus = 0, per_cu = 0;
-    static size_t lds_cached = ~(size_t)0;
     auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH, TASKS>;
-    if (cus == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorInvalidValue;
-    }
-    if (lds_cached != lds) {
-        if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-            return hipErrorInvalidValue;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess)
-            return hipErrorInvalidValue;
-        if (per_cu < 1) return hipErrorInvalidConfiguration;
-        lds_cached = lds;
-    }
+    int cus = 0, per_cu = 0;
+    const hipError_t oe = occupancy(reinterpret_cast<const void *>(kern), threads, lds, cus, per_cu);
+    if (oe != hipSuccess) return oe;
+    if (MAXD == 0 && LB > 1 && per_cu > RG_DEEP_BLOCKS_PER_CU) per_cu = RG_DEEP_BLOCKS_PER_CU;
     const unsigned long long tiles = (unsigned long long)((a->width + 7) / 8) * ((a->out_rows + 7) / 8);
     const unsigned long long waves = (unsigned long long)threads / 64u;
     unsigned long long blocks = (unsigned long long)cus * per_cu;
     const unsigned long long need = (tiles + waves - 1) / waves;
     if (blocks > need) blocks = need;
-    constexpr unsigned long long kmax = LB > 1 ? RG_LIGHT_TILES_PER_WAVE : RG_HEAVY_TILES_PER_WAVE;
+    constexpr unsigned long long kmax = MAXD == 0 ? 0 : LB > 1 ? RG_LIGHT_TILES_PER_WAVE : RG_HEAVY_TILES_PER_WAVE;
     if constexpr (kmax > 0)  // non-persistent: one wave per kmax tiles
         blocks = (tiles + waves * kmax - 1) / (waves * kmax);
     if (blocks < 1) blocks = 1;
+    if (grid_threads) {
+        *grid_threads = (size_t)blocks * threads;
+        return hipSuccess;
+    }
+    if (MAXD == 0 && (a->deep_stack == nullptr || (unsigned long long)a->deep_stride < blocks * threads))
+        return hipErrorInvalidValue;  // the caller sized the frame buffer for another grid
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), lds, stream, *a);
     return hipGetLastError();
 }
@@ -2133,15 +2247,15 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
 // RG_HEAVY_SCENE_BODIES and the path decision (rg_heavy_path) live in rg_device.h
 
 template <int MAXD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
-static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream) {
+static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t *gt) {
     // the BVH kernels also hold the static per-wave traversal stacks
     constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u) -
                                 (TASKS ? (uint32_t)sizeof(TaskPool) : 0u);
     if (a->lds_total_bytes <= budget)  // whole scene (empty sphere part if n_sph == 0)
-        return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS>(a, a->lds_total_bytes, stream);
+        return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS>(a, a->lds_total_bytes, stream, gt);
     if (a->n_sph > 0 && a->lds_hot_bytes <= budget)
-        return launch_one<MAXD, true, false, WPS, LB, F32F, BVH, TASKS>(a, a->lds_hot_bytes, stream);
-    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH, TASKS>(a, a->lds_lstack_bytes, stream);
+        return launch_one<MAXD, true, false, WPS, LB, F32F, BVH, TASKS>(a, a->lds_hot_bytes, stream, gt);
+    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH, TASKS>(a, a->lds_lstack_bytes, stream, gt);
 }
 
 #ifndef RG_LIGHT_WPS
@@ -2149,27 +2263,40 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream) {
 #endif
 
 template <int MAXD>
-static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream) {
+static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t *gt) {
     // Light scenes (few bodies): per-iteration overhead dominates -> fewer,
     // fatter iterations (RG_LB shadow rays per pass) at 2 waves/SIMD.  Heavy
     // scenes: the body loop dominates and waves mix ray kinds -> one ray per
     // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
     const bool heavy = rg_heavy_path(*a);
-    if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream);
+    if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream, gt);
     const unsigned long long tiles = (unsigned long long)((a->width + 7) / 8) * ((a->out_rows + 7) / 8);
     const bool tasks = RG_HEAVY_TASKS && tiles < RG_HEAVY_TASK_TILES;
     if (a->n_nodes > 0)
-        return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, true>(a, stream)
-                     : launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, false>(a, stream);
-    return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, true>(a, stream)
-                 : launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, false>(a, stream);
+        return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, true>(a, stream, gt)
+                     : launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, false>(a, stream, gt);
+    return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, true>(a, stream, gt)
+                 : launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, false>(a, stream, gt);
+}
+
+// Frame-stack capacity of each compiled array instantiation; deeper scenes use
+// the global frame buffer (MAXD == 0).
+extern "C" int rg_max_array_frames(void) { return 64; }
+
+static hipError_t dispatch_depth(const RgKernelArgs *a, int maxd, hipStream_t stream, size_t *gt) {
+    if (maxd <= 8) return launch_depth<8>(a, stream, gt);
+    if (maxd <= 16) return launch_depth<16>(a, stream, gt);
+    if (maxd <= 64) return launch_depth<64>(a, stream, gt);
+    return launch_depth<0>(a, stream, gt);
 }
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {
-    if (maxd <= 8) return launch_depth<8>(a, stream);
-    if (maxd <= 16) return launch_depth<16>(a, stream);
-    if (maxd <= 64) return launch_depth<64>(a, stream);
-    return hipErrorInvalidValue;
+    return dispatch_depth(a, maxd, stream, nullptr);
+}
+
+// Threads of the grid rg_launch_render would use (frame-buffer sizing for maxd > 64).
+extern "C" hipError_t rg_render_grid_threads(const RgKernelArgs *a, int maxd, size_t *threads) {
+    return dispatch_depth(a, maxd, nullptr, threads);
 }
 
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,

@@ -278,6 +278,10 @@ class DeviceScene:
         non-primary rays, large: none, -1: default) (include/raingun_debug.h)."""
         _abi.check(_abi.lib().rg_debug_set_lane_depth(self.handle, int(min_depth)))
 
+    def set_image_bands(self, bands: int) -> None:
+        """Row bands of host-visible renders (0: by frame size; include/raingun_debug.h)."""
+        _abi.check(_abi.lib().rg_debug_set_image_bands(self.handle, int(bands)))
+
     def bvh_info(self) -> _abi.rg_bvh_info:
         info = _abi.rg_bvh_info()
         _abi.check(_abi.lib().rg_debug_bvh_info(self.handle, C.byref(info)))
@@ -286,12 +290,51 @@ class DeviceScene:
     def set_max_depth(self, depth: int) -> None:
         _abi.check(_abi.lib().rg_scene_set_max_depth(self.handle, int(depth)))
 
-    def render_image(self, width: int, height: int, stats: Optional[_abi.rg_stats] = None) -> np.ndarray:
-        out = np.empty((height, width, 4), dtype=np.uint8)
+    def render_image(self, width: int, height: int, stats: Optional[_abi.rg_stats] = None,
+                     out: Optional[np.ndarray] = None) -> np.ndarray:
+        """rendering::render_image (rendering.rs:24-38) into host memory.  `out`
+        (optional, (height, width, 4) uint8, C-contiguous) may be a buffer
+        registered with register_host() for direct DMA."""
+        if out is None:
+            out = np.empty((height, width, 4), dtype=np.uint8)
+        assert out.shape == (height, width, 4) and out.dtype == np.uint8 and out.flags.c_contiguous
         st = stats if stats is not None else _abi.rg_stats()
         _abi.check(_abi.lib().rg_render_image(self.handle, width, height, out.ctypes.data, C.byref(st)),
                    "rg_render_image")
         return out
+
+    def render_multi(self, width: int, height: int, ngpus: int, tile_rows: int = 0,
+                     stats: Optional[_abi.rg_stats] = None, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """rg_render_multi: the frame over `ngpus` devices of this process (row
+        tiles, one RCCL gather to this scene's device), delivered to host memory."""
+        if out is None:
+            out = np.empty((height, width, 4), dtype=np.uint8)
+        st = stats if stats is not None else _abi.rg_stats()
+        _abi.check(_abi.lib().rg_render_multi(self.handle, width, height, int(ngpus), int(tile_rows),
+                                              out.ctypes.data, C.byref(st)), "rg_render_multi")
+        return out
+
+    def render_stream(self, width: int, height: int, on_tile, tile_rows: int = 16,
+                      stats: Optional[_abi.rg_stats] = None) -> int:
+        """rg_render_stream: on_tile(row0, band) gets each band of finished RGBA8
+        rows (a copy); return True to cancel.  Returns the rg_status."""
+        st = stats if stats is not None else _abi.rg_stats()
+
+        def cb(row0, rows, w, ptr, _user):
+            band = np.ctypeslib.as_array(ptr, shape=(rows * w * 4,)).reshape(rows, w, 4).copy()
+            return 1 if on_tile(int(row0), band) else 0
+
+        fn = _abi.TILE_CALLBACK(cb)
+        return _abi.lib().rg_render_stream(self.handle, width, height, tile_rows, fn, None, C.byref(st))
+
+    def stream_status(self, stream: int):
+        """(status, error_pixel) of the launches on `stream` (a hipStream_t value) since the last call."""
+        px = C.c_int32(-1)
+        st = _abi.lib().rg_stream_status(self.handle, C.c_void_p(stream), C.byref(px))
+        return st, px.value
+
+    def release_stream(self, stream: int) -> None:
+        _abi.check(_abi.lib().rg_scene_release_stream(self.handle, C.c_void_p(stream)), "rg_scene_release_stream")
 
     def render_tiles(self, width: int, height: int, tile_rows: int = 0, stride: int = 1, offset: int = 0,
                      want_rgb: bool = False, stats: Optional[_abi.rg_stats] = None):
@@ -345,15 +388,8 @@ class Scene:                   # scene.rs:11-31
                          tile_rows: int = 16, device: int = 0) -> _abi.rg_stats:
         ds = DeviceScene(self, device)
         stats = _abi.rg_stats()
-
-        def cb(row0, rows, w, ptr, _user):
-            band = np.ctypeslib.as_array(ptr, shape=(rows * w * 4,)).reshape(rows, w, 4).copy()
-            return 1 if on_tile(int(row0), band) else 0
-
-        fn = _abi.TILE_CALLBACK(cb)
         try:
-            _abi.check(_abi.lib().rg_render_stream(ds.handle, width, height, tile_rows, fn, None, C.byref(stats)),
-                       "rg_render_stream")
+            _abi.check(ds.render_stream(width, height, on_tile, tile_rows, stats), "rg_render_stream")
         finally:
             ds.close()
         return stats

@@ -3,6 +3,7 @@ a world-1 RCCL process group runs the same per-frame loop an N-GPU node runs
 (render on stream k % depth, ncclGather on the communication stream, rank 0's
 re-interleave on a side stream).  Every delivered frame must equal a one-shot
 render byte for byte."""
+import ctypes as C
 import os
 import socket
 
@@ -47,4 +48,107 @@ def test_native_pipeline_frames_equal_one_shot_render(nccl_world1, example_scene
     pipe.flush()
     assert np.array_equal(pipe.read_frame(), ref)
     pipe.close()
+    ds.close()
+
+
+# ncclGather's signature (rccl.h:745) as rg_gather_fn (include/raingun_frames.h)
+GATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_void_p, C.c_void_p)
+
+
+def _hip_runtime():
+    """The HIP runtime PyTorch loaded (the instance libraingun_hip.so binds to)."""
+    import torch
+
+    hip = C.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    hip.hipMemcpyAsync.restype = C.c_int
+    hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+    return hip
+
+
+def _fake_gather(world, others, calls):
+    """A stand-in for ncclGather on rank 0 of `world` ranks: slot 0 of the
+    receive buffer gets this rank's part, slot r the pre-rendered part of rank
+    r -- device copies on the stream the pipeline hands over, as RCCL would."""
+    hip = _hip_runtime()
+
+    def gather(send, recv, count, dtype, root, comm, stream):
+        assert dtype == 1 and root == 0 and recv
+        calls.append(count)
+        if hip.hipMemcpyAsync(recv, send, count, 3, stream) != 0:  # hipMemcpyDeviceToDevice
+            return 1
+        for r in range(1, world):
+            if hip.hipMemcpyAsync(recv + r * count, others[r].data_ptr(), count, 3, stream) != 0:
+                return 1
+        return 0
+
+    return GATHER_FN(gather)
+
+
+@pytest.mark.parametrize("world,w,h,T,depth", [(2, 320, 243, 8, 3), (3, 256, 144, 16, 2), (8, 640, 357, 8, 4),
+                                               (8, 97, 61, 8, 1)])
+def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, depth):
+    """The N > 1 native loop on one GPU: rank 0 of `world` ranks,
+    the other ranks' parts (tiling {T, world, r}) pre-rendered and delivered by
+    a stand-in gather.  The re-interleave, the slot offsets and the padding of
+    heights that are not a multiple of T all run; every frame equals the
+    one-shot render byte for byte."""
+    import torch
+
+    from raingun_amd import _abi
+
+    ds = DeviceScene(example_scenes["test1"])
+    ref = ds.render_image(w, h)
+    lib = _abi.lib()
+    slot = rd.slot_rows(h, world, T)
+    others = [torch.zeros((slot, w, 4), dtype=torch.uint8, device="cuda") for _ in range(world)]
+    for r in range(1, world):
+        t = _abi.rg_tiling(T, world, r)
+        _abi.check(lib.rg_render_tiles_async(ds.handle, w, h, C.byref(t), C.c_void_p(others[r].data_ptr()), None,
+                                             None, None))
+    torch.cuda.synchronize()
+    calls = []
+    fn = _fake_gather(world, others, calls)
+    hdl = C.c_void_p()
+    _abi.check(lib.rg_frames_create(ds.handle, w, h, T, 0, world, depth, C.c_void_p(1), C.cast(fn, C.c_void_p),
+                                    C.byref(hdl)))
+    out = np.empty((h, w, 4), np.uint8)
+    for k in range(2 * depth + 1):
+        _abi.check(lib.rg_frames_step(hdl))
+        if k % 2 == 0:
+            _abi.check(lib.rg_frames_read_image(hdl, out.ctypes.data))
+            assert np.array_equal(out, ref), k
+    _abi.check(lib.rg_frames_flush(hdl))
+    lib.rg_frames_destroy(hdl)
+    ds.close()
+    assert calls and all(c == slot * w * 4 for c in calls)
+
+
+def test_native_pipeline_reports_device_errors():
+    """a frame that raises a device error (the AABB-normal panic,
+    bodies.rs:324) is still delivered, and rg_frames_flush / _status /
+    _read_image report the error and its first pixel."""
+    from raingun_amd import _abi
+    from raingun_amd.color import Color
+    from raingun_amd.scene import AABB, Material, Scene
+
+    m = Material(Color.from_str("#ffffff"), 0.5)
+    bad = Scene(bodies=[AABB(((-3e8, -3e8, -7e8), (3e8, 3e8, -5e8)), m)])
+    ds = DeviceScene(bad)
+    st = _abi.rg_stats()
+    with pytest.raises(_abi.RaingunError):
+        ds.render_tiles(64, 48, stats=st)
+    lib = _abi.lib()
+    calls = []
+    fn = _fake_gather(1, [None], calls)
+    hdl = C.c_void_p()
+    _abi.check(lib.rg_frames_create(ds.handle, 64, 48, 8, 0, 1, 2, C.c_void_p(1), C.cast(fn, C.c_void_p),
+                                    C.byref(hdl)))
+    for _ in range(3):
+        _abi.check(lib.rg_frames_step(hdl))
+    px = C.c_int32(-2)
+    assert lib.rg_frames_status(hdl, C.byref(px)) == _abi.RG_ERR_AABB_NORMAL
+    assert px.value == st.error_pixel
+    out = np.empty((48, 64, 4), np.uint8)
+    assert lib.rg_frames_read_image(hdl, out.ctypes.data) == _abi.RG_ERR_AABB_NORMAL
+    lib.rg_frames_destroy(hdl)
     ds.close()

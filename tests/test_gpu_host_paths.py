@@ -1,0 +1,305 @@
+"""The host-facing entry points of the C ABI against the CPU restatement:
+host-visible frames (rg_render_image: banded renders overlapped with their
+copies, pageable and page-locked buffers), tile streaming with real double
+buffering (rg_render_stream), the single-process multi-GPU entry
+(rg_render_multi), recursion deeper than the compiled frame arrays, and the
+reference's panic sites as status codes (scene.rs:38 NaN distance for
+closest-hit AND shadow rays, rendering.rs:106 transmission, bodies.rs:324
+AABB normal) -- status and first pixel equal to the restatement's.
+"""
+import ctypes as C
+import time
+
+import numpy as np
+import pytest
+
+from raingun_amd import _abi
+from raingun_amd.color import Color
+from raingun_amd.scene import (AABB, DeviceScene, DirectionalLight, Material, Plane, Scene, SceneDesc, Sphere,
+                               SphericalLight)
+from raingun_amd.synth import synthetic_scene
+
+pytestmark = pytest.mark.gpu
+
+RGB_TOL = 1e-4
+WHITE = Color.from_str("#ffffff")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    assert _abi.lib().rg_device_count() > 0, "no HIP device visible"
+
+
+def _oracle(oracle_lib, scene, w, h):
+    st, rgba, rgb, counts, err = oracle_lib.render(SceneDesc(scene), w, h, want_rgb=True)
+    return st, rgba, rgb, counts, err
+
+
+# ---------------------------------------------------------------- host-visible frames
+@pytest.mark.parametrize("bands", [1, 2, 3, 7])
+@pytest.mark.parametrize("kind,w,h", [("test1", 800, 600), ("synth200", 640, 360), ("test2", 97, 61),
+                                      ("test3", 33, 9)])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_render_image_host_visible(oracle_lib, example_scenes, kind, w, h, bands, pinned):
+    scene = synthetic_scene(200, 2, 5) if kind == "synth200" else example_scenes[kind]
+    o_st, o_rgba, _, o_counts, _ = _oracle(oracle_lib, scene, w, h)
+    assert o_st == 0
+    ds = DeviceScene(scene)
+    ds.set_image_bands(bands)
+    out = np.full((h, w, 4), 123, dtype=np.uint8)
+    reg = _abi.HostRegistration(out) if pinned else None
+    try:
+        for _ in range(2):  # the scene's framebuffer / staging are reused across calls
+            st = _abi.rg_stats()
+            got = ds.render_image(w, h, stats=st, out=out)
+            assert np.array_equal(got, o_rgba)
+            assert st.rays.as_dict() == o_counts
+            assert st.error_pixel == -1
+    finally:
+        if reg is not None:
+            reg.close()
+        ds.close()
+
+
+def test_render_image_4k_default_bands(oracle_lib, example_scenes):
+    """BASELINE configs[1] through the drop-in itself: test1 3840x2160 depth 5,
+    host-visible, the library's default band count."""
+    import copy
+
+    s = copy.copy(example_scenes["test1"])
+    s.max_recursion_depth = 5
+    o_st, o_rgba, _, o_counts, _ = _oracle(oracle_lib, s, 3840, 2160)
+    ds = DeviceScene(s)
+    st = _abi.rg_stats()
+    got = ds.render_image(3840, 2160, stats=st)
+    ds.close()
+    assert np.array_equal(got, o_rgba)
+    assert st.rays.as_dict() == o_counts
+
+
+@pytest.mark.parametrize("tile_rows,stride,offset", [(8, 3, 1), (600, 1, 0), (7, 1, 0), (5, 2, 1)])
+def test_render_tiles_rgb_host(oracle_lib, example_scenes, tile_rows, stride, offset):
+    """rg_render_tiles (host buffers, f32 RGB too): a whole-frame tiling is
+    banded, a sharded one is one launch; padding rows come back zeroed."""
+    s = example_scenes["test1"]
+    w, h = 320, 243
+    ds = DeviceScene(s)
+    ds.set_image_bands(3)
+    rgba, rgb = ds.render_tiles(w, h, tile_rows, stride, offset, want_rgb=True)
+    ds.close()
+    o_st, o_rgba, o_rgb, _, _ = oracle_lib.render(SceneDesc(s), w, h, tile_rows, stride, offset, want_rgb=True)
+    assert o_st == 0
+    assert np.array_equal(rgba, o_rgba)
+    assert float(np.abs(rgb - o_rgb).max()) <= RGB_TOL
+
+
+# ---------------------------------------------------------------- streaming
+@pytest.mark.parametrize("tile_rows", [32, 37, 240, 1])
+def test_stream_bands_match_oracle(oracle_lib, example_scenes, tile_rows):
+    """render_image_stream (rendering.rs:40-69) as tile callbacks: every band
+    equals the CPU restatement's rows; a slow callback overlaps later bands'
+    renders and copies (the bands still arrive in order, complete)."""
+    s = example_scenes["test1"]
+    w, h = 320, 240
+    o_st, o_rgba, _, o_counts, _ = _oracle(oracle_lib, s, w, h)
+    got = np.zeros_like(o_rgba)
+    seen = []
+
+    def on_tile(row0, band):
+        if len(seen) < 4:
+            time.sleep(0.002)
+        got[row0:row0 + band.shape[0]] = band
+        seen.append((row0, band.shape[0]))
+        return False
+
+    ds = DeviceScene(s)
+    st = _abi.rg_stats()
+    _abi.check(ds.render_stream(w, h, on_tile, tile_rows, st))
+    ds.close()
+    assert np.array_equal(got, o_rgba)
+    assert [r for r, _ in seen] == list(range(0, h, tile_rows))
+    assert sum(n for _, n in seen) == h
+    assert st.rays.as_dict() == o_counts
+
+
+def test_stream_cancel_after_two_bands(example_scenes):
+    s = example_scenes["test2"]
+    calls = []
+    ds = DeviceScene(s)
+    status = ds.render_stream(320, 240, lambda r, b: calls.append(r) or len(calls) == 2, 32)
+    # the scene stays usable after a cancelled stream
+    full = ds.render_image(320, 240)
+    ds.close()
+    assert status == _abi.RG_ERR_CANCELLED
+    assert calls == [0, 32]
+    assert full.shape == (240, 320, 4)
+
+
+# ---------------------------------------------------------------- panic sites
+def _far_sphere_scene(fov, with_ceiling=True):
+    """A sphere at 5e154: for a ray whose direction has a large component along
+    it, h.h and adj^2 both overflow and opp = inf - inf is NaN (bodies.rs:95),
+    so the sphere 'hits' at NaN.  Scene::trace panics (scene.rs:38) when a ray
+    has another hit besides.  fov 90: the primary rays of the top rows already
+    do; fov 30: only the shadow rays towards the light overhead do."""
+    m = Material(WHITE, 0.5)
+    bodies = [Sphere((0.0, 5e154, 0.0), 1.0, m), Plane((0.0, -2.0, 0.0), (0.0, -1.0, 0.0), m)]
+    if with_ceiling:
+        bodies.append(Plane((0.0, 10.0, 0.0), (0.0, 1.0, 0.0), m))
+    return Scene(fov=fov, bodies=bodies, lights=[DirectionalLight((0.0, -1.0, 0.0), WHITE, 1.0)])
+
+
+def _error_case(oracle_lib, scene, w, h, path):
+    o_st, o_rgba, _, o_counts, o_err = _oracle(oracle_lib, scene, w, h)
+    ds = DeviceScene(scene, path=path)
+    st = _abi.rg_stats()
+    out = np.zeros((h, w, 4), np.uint8)
+    status = _abi.lib().rg_render_image(ds.handle, w, h, out.ctypes.data, C.byref(st))
+    ds.close()
+    assert status == o_st, (status, o_st)
+    assert st.error_pixel == o_err
+    assert st.rays.as_dict() == o_counts
+    assert np.array_equal(out, o_rgba)  # the frame is delivered either way
+    return status
+
+
+PATHS = [_abi.PATH_LIGHT, _abi.PATH_HEAVY]
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_nan_distance_closest_hit(oracle_lib, path):
+    assert _error_case(oracle_lib, _far_sphere_scene(90.0), 5, 3, path) == _abi.RG_ERR_NAN_DISTANCE
+
+
+@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("w,h", [(5, 3), (64, 36)])
+def test_nan_distance_shadow_ray(oracle_lib, path, w, h):
+    """Primary rays see no NaN (fov 30); shadow rays towards the overhead light
+    see the NaN sphere and the ceiling: the reference panics in shade_diffuse's
+    trace (rendering.rs:150 -> scene.rs:38)."""
+    scene = _far_sphere_scene(30.0)
+    # the primary rays alone do not panic
+    rays = []
+    import oracle
+
+    fa = oracle.lib().rgo_fov_adjustment(30.0)
+    for y in range(h):
+        for x in range(w):
+            d = np.array([(((x + 0.5) / w) * 2 - 1) * (w / h) * fa, (1 - ((y + 0.5) / h) * 2) * fa, -1.0])
+            rays.append([0.0, 0.0, 0.0, *(d / np.linalg.norm(d))])
+    assert oracle_lib.trace(SceneDesc(scene), np.array(rays))[0] == 0
+    assert _error_case(oracle_lib, scene, w, h, path) == _abi.RG_ERR_NAN_DISTANCE
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_nan_distance_single_hit_shadow_is_occluded(oracle_lib, path):
+    """A shadow ray whose only hit is at NaN: min_by compares nothing, no panic,
+    and `dist > light distance` is false -> in shadow (rendering.rs:152-155)."""
+    assert _error_case(oracle_lib, _far_sphere_scene(30.0, with_ceiling=False), 16, 9, path) == _abi.RG_OK
+
+
+@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("w,h", [(5, 3), (33, 21)])
+def test_transmission_none_while_kr_below_one(oracle_lib, path, w, h):
+    """An odd width puts a primary ray at d.x == 0 exactly; it hits the +z face
+    of a refractive box whose -x face is 5e-9 from x = 0, so the face search
+    (bodies.rs:311-327) returns the -x normal and i.n == 0: fresnel sees the
+    outside (kr < 1), create_transmission the inside with k < 0 -> None ->
+    unwrap panics (rendering.rs:106)."""
+    glass = Material(WHITE, 0.5, "Refractive", 0.0, 1.5, 0.8)
+    m = Material(WHITE, 0.5)
+    scene = Scene(bodies=[AABB(((-5e-9, -1.0, -5.0), (1.0, 1.0, -3.0)), glass),
+                          Plane((0.0, -2.0, 0.0), (0.0, -1.0, 0.0), m)],
+                  lights=[DirectionalLight((0.0, -1.0, 0.0), WHITE, 1.0)])
+    assert _error_case(oracle_lib, scene, w, h, path) == _abi.RG_ERR_TRANSMISSION
+
+
+def test_aabb_normal_error_through_stream_status():
+    """Asynchronous launches report nothing themselves; rg_stream_status returns
+    the first error any launch on the stream raised, then clears it."""
+    import torch
+
+    m = Material(WHITE, 0.5)
+    bad = Scene(bodies=[AABB(((-3e8, -3e8, -7e8), (3e8, 3e8, -5e8)), m)])
+    ds = DeviceScene(bad)
+    lib = _abi.lib()
+    stream = torch.cuda.Stream()
+    buf = torch.empty((48, 64, 4), dtype=torch.uint8, device="cuda")
+    t = _abi.rg_tiling(48, 1, 0)
+    for _ in range(3):
+        _abi.check(lib.rg_render_tiles_async(ds.handle, 64, 48, C.byref(t), C.c_void_p(buf.data_ptr()), None,
+                                             C.c_void_p(stream.cuda_stream), None))
+    status, pixel = ds.stream_status(stream.cuda_stream)
+    assert status == _abi.RG_ERR_AABB_NORMAL and pixel >= 0
+    assert ds.stream_status(stream.cuda_stream) == (_abi.RG_OK, -1)  # cleared
+    ds.release_stream(stream.cuda_stream)
+    ds.close()
+
+
+# ---------------------------------------------------------------- deep recursion
+def _mirror_corridor(depth):
+    """Two facing one-sided reflecting planes (behind and in front of the
+    camera): every primary ray bounces until max_recursion_depth."""
+    mirror = Material(Color.from_str("#a0c0ff"), 0.6, "Reflecting", 0.9)
+    ball = Material(Color.from_str("#ff8040"), 0.5, "Reflecting", 0.3)
+    return Scene(max_recursion_depth=depth,
+                 bodies=[Plane((0.0, 0.0, -10.0), (0.0, 0.0, -1.0), mirror),
+                         Plane((0.0, 0.0, 10.0), (0.0, 0.0, 1.0), mirror),
+                         Sphere((1.0, 0.5, -6.0), 1.0, ball),
+                         Plane((0.0, -3.0, 0.0), (0.0, -1.0, 0.0), Material(WHITE, 0.4))],
+                 lights=[SphericalLight((0.0, 4.0, 0.0), WHITE, 400.0),
+                         DirectionalLight((0.3, -1.0, -0.2), WHITE, 0.5)])
+
+
+@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("depth", [66, 100, 300])
+def test_recursion_deeper_than_compiled_frames(oracle_lib, path, depth):
+    """scene.rs:16 is a u32 and rendering.rs:122-130 recurses until it: depths
+    above 65 keep their shading frames in device memory (FrameStack<0>)."""
+    scene = _mirror_corridor(depth)
+    w, h = 64, 36
+    o_st, o_rgba, o_rgb, o_counts, _ = _oracle(oracle_lib, scene, w, h)
+    assert o_st == 0
+    assert o_counts["secondary"] >= w * h * (depth - 1) // 3  # the chains really are deep
+    ds = DeviceScene(scene, path=path)
+    st = _abi.rg_stats()
+    rgba, rgb = ds.render_tiles(w, h, want_rgb=True, stats=st)
+    ds.close()
+    assert st.rays.as_dict() == o_counts
+    assert np.array_equal(rgba, o_rgba)
+    assert float(np.abs(rgb - o_rgb).max()) <= RGB_TOL
+
+
+# ---------------------------------------------------------------- rg_render_multi
+@pytest.mark.parametrize("kind,w,h,tile_rows", [("test1", 320, 243, 8), ("synth200", 256, 144, 16),
+                                                ("test3", 97, 61, 0)])
+def test_render_multi_one_device(oracle_lib, example_scenes, kind, w, h, tile_rows):
+    """The single-process multi-GPU entry at ngpus = 1: replicas, ncclCommInitAll,
+    the gather to device 0 and the re-interleave all run (a 1-rank gather)."""
+    import torch
+
+    scene = synthetic_scene(200, 2, 5) if kind == "synth200" else example_scenes[kind]
+    o_st, o_rgba, _, o_counts, _ = _oracle(oracle_lib, scene, w, h)
+    ds = DeviceScene(scene)
+    for _ in range(2):
+        st = _abi.rg_stats()
+        got = ds.render_multi(w, h, 1, tile_rows, stats=st)
+        assert np.array_equal(got, o_rgba)
+        assert st.rays.as_dict() == o_counts
+    ngpu = torch.cuda.device_count()
+    with pytest.raises(_abi.RaingunError) as ei:
+        ds.render_multi(w, h, ngpu + 1)
+    assert ei.value.status == _abi.RG_ERR_INVALID_ARGUMENT
+    ds.close()
+
+
+def test_render_multi_reports_device_errors(oracle_lib):
+    scene = _far_sphere_scene(30.0)
+    o_st, _, _, _, o_err = _oracle(oracle_lib, scene, 64, 36)
+    ds = DeviceScene(scene)
+    st = _abi.rg_stats()
+    out = np.zeros((36, 64, 4), np.uint8)
+    status = _abi.lib().rg_render_multi(ds.handle, 64, 36, 1, 8, out.ctypes.data, C.byref(st))
+    ds.close()
+    assert status == o_st == _abi.RG_ERR_NAN_DISTANCE
+    assert st.error_pixel == o_err
