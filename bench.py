@@ -3,23 +3,31 @@
 
 One step = one frame of the workload rendered by the HIP megakernel, scene and
 textures already resident in HBM, framebuffer left in HBM (rank 0 holds the
-assembled frame).  At N>1 (torchrun, one rank per GPU) the frame is cut into
-8-row tiles dealt round-robin to the ranks and the tiles are gathered to rank
-0 with one RCCL gather per frame (ncclGather on the communicator of the
-torch.distributed "nccl" group, i.e. RCCL over xGMI), then re-interleaved into
-image order on rank 0 -- the per-frame loop runs in C++ (include/raingun_frames.h).
+assembled frame).  At N>1 (one rank per GPU: torchrun, or `--gpus N`, which
+launches torch.distributed.run itself) the frame is cut into 8-row tiles dealt
+round-robin to the ranks and the tiles are gathered to rank 0 with one RCCL
+gather per frame (ncclGather on the communicator of the torch.distributed
+"nccl" group, i.e. RCCL over xGMI), then re-interleaved into image order on
+rank 0 -- the per-frame loop runs in C++ (include/raingun_frames.h).
 
 Workload (BASELINE.json configs[1]): examples/test1.yml at 3840x2160,
-recursion depth 5, 1 GPU.  `--workload synth1024` selects the north_star's
-1024-sphere 3840x2160 depth-5 scene instead.  Two extra line items report the
-north_star scene at 3840x2160 and at 7680x4320 (BASELINE configs[3]) on the
-same N GPUs.  Frames are kept in flight (4, each on its own render stream):
-the timed region holds `--steps` complete frames.
+recursion depth 5.  Extra line items on the same N GPUs: configs[2]
+(test3.yml 3840x2160), the north_star scene (1024 spheres, 3840x2160, depth
+5), configs[3] (the same at 7680x4320) and configs[4] (4096 spheres + 8
+planes, 16384x16384, depth 8); at N=1 `host_visible` times the drop-in itself,
+rg_render_image, with the frame in host memory when each call returns.
+Frames are kept in flight (6, each on its own render stream): the timed
+region holds `--steps` complete frames (fewer for the slow extra lines, see
+`steps` in each).
 
-Prints ONE JSON line on rank 0 (the driver's contract) with `roofline`
-(FP64-VALU bound, from HIP events on the render stream), `roofline_hbm`
-(achieved HBM bytes, as the north_star asks) and `cpu_baseline` (the CPU
-restatement in oracle/, timed on this host's cores on a bounded sample).
+Prints ONE JSON line on rank 0 (the driver's contract).  `roofline` is the
+executed-work VALU roofline: issue cycles of the instructions the kernels
+executed per frame (rocprofv3 PMC, profiles/pmc_work.json: FP64 4 cycles, f32
+transcendental 4, every other VALU instruction 2 per wave64 on a 32-lane
+SIMD; MI355X_MICROARCH.md) over 1,024 SIMDs x 2.4 GHz x the measured time per
+frame, as FP64-rate lane-ops/s against 39.3 T.  `roofline_hbm` reports HBM
+bytes; `cpu_baseline` the CPU restatement in oracle/ on this host's cores on a
+bounded sample.
 """
 from __future__ import annotations
 
@@ -27,6 +35,8 @@ import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -36,6 +46,7 @@ sys.path.insert(0, str(REPO))
 
 METRIC = "Mrays/sec (primary+shadow+secondary) at 3840×2160, depth 5; 1/2/4/8 MI355X"
 FP64_PEAK_TOPS = 39.3     # MI355X FP64 vector 78.6 TFLOP/s spec counts FMA as 2; parity forbids FMA -> 39.3 T ops/s
+SIMDS, CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMDs; peak engine clock (39.3 T = 1024 x 16 FP64 lanes x 2.4 GHz)
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 # Algorithmic FP64 ops per body test on the reference's miss path.
 OPS_PER_BODY = {"sphere": 16, "plane": 14, "disk": 20, "aabb": 18}
@@ -59,12 +70,22 @@ def load_workload(name: str, W: int = 3840, H: int = 2160):
         src = ("reference example scene examples/test3.yml; textures decoded by the native host layer "
                "(libraingun_host.so, jpeg-decoder 0.1.11 rounding)")
     elif name.startswith("synth"):
-        n = int(name[5:] or 1024)
-        text = synthetic_yaml(n, 2, 5)
+        import re
+
+        m = re.fullmatch(r"synth(\d*)(?:p(\d+))?(?:d(\d+))?", name)
+        if not m:
+            raise SystemExit(f"unknown workload {name}")
+        n, planes, depth = int(m.group(1) or 1024), int(m.group(2) or 2), int(m.group(3) or 5)
+        text = synthetic_yaml(n, planes, depth)
         scene = load_scene(text)
-        label = f"synthetic {n} spheres + 2 planes {W}x{H} depth 5 (seed 0x5EED, md5 {scene_md5(text)})"
-        if (W, H) == (7680, 4320):
+        label = (f"synthetic {n} spheres + {planes} planes {W}x{H} depth {depth} "
+                 f"(seed 0x5EED, md5 {scene_md5(text)})")
+        if (n, planes, depth, W, H) == (1024, 2, 5, 7680, 4320):
             label += " (BASELINE configs[3])"
+        elif (n, planes, depth, W, H) == (4096, 8, 8, 16384, 16384):
+            label += " (BASELINE configs[4])"
+        elif (n, planes, depth, W, H) == (1024, 2, 5, 3840, 2160):
+            label += " (north_star)"
         src = "synthetic seeded scene (raingun_amd/synth.py)"
     else:
         raise SystemExit(f"unknown workload {name}")
@@ -96,16 +117,16 @@ def cpu_baseline(scene, width, height, budget_s: float = 12.0):
     desc = SceneDesc(scene)
     threads = oracle.default_threads()
     tiles = (height + TILE_ROWS - 1) // TILE_ROWS
-    stride = 1  # first probe: the whole frame
+    stride = max(1, tiles // 64) if width * height > 40_000_000 else 1  # first probe: the whole frame (or 64 tiles)
     while True:
         t0 = time.perf_counter()
         st, _, _, counts, _ = oracle.render(desc, width, height, TILE_ROWS, stride, 0, threads=threads)
         dt = time.perf_counter() - t0
         if st != 0:
             raise RuntimeError(f"oracle status {st}")
-        if dt * stride <= budget_s or stride >= tiles:
+        if dt <= budget_s or stride >= tiles:
             break
-        stride = min(tiles, int(stride * (dt * stride / budget_s)) + 1)
+        stride = min(tiles, int(stride * dt / budget_s * 2) + 1)
     reps, elapsed, rays = 1, dt, sum(counts.values())
     while elapsed < budget_s / 2 and reps < 100:
         t0 = time.perf_counter()
@@ -124,22 +145,56 @@ def cpu_baseline(scene, width, height, budget_s: float = 12.0):
     }
 
 
-def load_traffic(workload: str, n_gpus: int, key: str = "hbm_bytes_per_launch"):
-    """A PMC figure for this workload's kernel (scripts/pmc.sh -> profiles/traffic.json)."""
-    f = REPO / "profiles" / "traffic.json"
-    if n_gpus != 1 or not f.exists():
+def pmc_work(key: str):
+    """Executed work per frame of one workload (scripts/pmc_work.py -> profiles/pmc_work.json):
+    VALU issue cycles, HBM bytes, instruction mix; None if not profiled."""
+    f = REPO / "profiles" / "pmc_work.json"
+    if not f.exists():
         return None
     try:
-        d = json.loads(f.read_text())
-        return d.get(workload, {}).get(key)
+        return json.loads(f.read_text()).get(key)
     except Exception:
         return None
 
 
-def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cpu: bool, size=None):
-    """Time `args.steps` frames of `workload` on this rank (after `args.warmup`),
-    frame sharded over `world` ranks and gathered to rank 0.  Returns the
-    rank-0 result dict (None on other ranks)."""
+def roofline(key: str, frame_s: float, n_gpus: int, alg_bytes: int, tex: int):
+    """Executed-work VALU roofline of the timed configuration: the issue cycles
+    of every VALU instruction the frame's kernels executed (PMC, counted at
+    N=1 for the whole frame, which the N ranks split) over the cycles N GPUs
+    offer in the measured time per frame."""
+    w = pmc_work(key)
+    res = {"bound": "valu", "achieved": None, "peak": round(FP64_PEAK_TOPS * n_gpus, 3),
+           "unit": "T FP64-rate VALU lane-ops/s", "frac": None, "traffic": None,
+           "basis": "not profiled (run scripts/pmc_work.sh for this workload)"}
+    if w:
+        cyc = w["valu_cycles_per_frame"]
+        frac = cyc / (frame_s * n_gpus * SIMDS * CLOCK_HZ)
+        res.update({
+            "achieved": round(cyc * 16.0 / frame_s / 1e12, 4),
+            "frac": round(frac, 5),
+            "traffic": w.get("hbm_bytes_per_frame"),
+            "valu_cycles_per_frame": cyc,
+            "basis": (f"executed work: {w['valu_insts_per_frame']:.4g} VALU wave64 instructions per frame "
+                      f"({w['f64_insts_per_frame']:.4g} FP64 x 4 cycles, {w['trans32_insts_per_frame']:.4g} f32 "
+                      f"transcendental x 4, the rest x 2 cycles on a 32-lane SIMD: MI355X_MICROARCH.md) = "
+                      f"{cyc:.4g} SIMD issue cycles per frame, over {SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz x "
+                      f"{n_gpus} GPU(s) x the measured {frame_s * 1e3:.4f} ms per frame (ms_per_step); "
+                      f"achieved = cycles x 16 FP64 lanes / time.  Counters: {w['source']}"),
+        })
+    hbm = {"bound": "hbm", "achieved": round(alg_bytes / frame_s / 1e9, 3), "peak": 8000.0 * n_gpus, "unit": "GB/s",
+           "frac": round(alg_bytes / frame_s / 1e9 / (8000.0 * n_gpus), 7),
+           "traffic": w.get("hbm_bytes_per_frame") if w else None,
+           "basis": f"{alg_bytes} B framebuffer written per frame (+{tex} B of textures read, L2/MALL resident) / "
+                    f"ms_per_step; traffic = PMC FETCH_SIZE x 2 + WRITE_SIZE (KiB -> B, gfx950 correction)"}
+    return res, hbm
+
+
+def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cpu: bool, size=None,
+            steps=None, warmup=None, budget_s=None):
+    """Time `steps` frames of `workload` on this rank (after `warmup`), frame
+    sharded over `world` ranks and gathered to rank 0.  `budget_s`: cap the
+    frames so the timed region lasts about that long (slow extra lines).
+    Returns the rank-0 result dict (None on other ranks)."""
     import torch
     import torch.distributed as dist
 
@@ -148,6 +203,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     from raingun_amd.scene import DeviceScene
 
     W, H = size or (args.width, args.height)
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
     scene, label, src, body_counts, ops_per_ray = load_workload(workload, W, H)
     ds = DeviceScene(scene, device=local_rank)  # scene + textures uploaded once, resident in HBM
     if args.tile_order >= 0:
@@ -166,6 +223,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     # process, see main): 6 -- the whole frame is flat from 4 up, a 1/8 test1
     # share gains 12 % from 4 to 6 (profiles/r01/bench_frames_in_flight_ab.txt)
     F = args.frames_in_flight if args.frames_in_flight > 0 else 6
+    if W * H >= 100_000_000:
+        F = min(F, 3)  # 1 GB frames (configs[4]): three in flight fill the GPU as well
     use_pipe = args.backend == "nccl" or world == 1
     gathered = rd.gather_buffers(out, world) if (world > 1 and rank == 0 and not use_pipe) else None
     frame = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if (rank == 0 and not use_pipe) else None
@@ -216,7 +275,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
 
     def finish():
         if pipe is not None:
-            pipe.flush()
+            pipe.flush()  # the native pipeline raises on a device error of any frame
 
     # one counted render: ray totals per class (deterministic per frame)
     stats = _abi.rg_stats()
@@ -228,16 +287,23 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     rays = [int(x) for x in rays.tolist()]
     rays_per_frame = sum(rays)
 
-    for _ in range(args.warmup):
+    t_w = time.perf_counter()
+    for _ in range(warmup):
         step()
     finish()
     torch.cuda.synchronize(dev)
+    t_w = (time.perf_counter() - t_w) / max(1, warmup)
+    if budget_s is not None and warmup > 0:  # slow lines: as many frames as fit the budget (same on every rank)
+        k = torch.tensor([max(3, min(steps, int(budget_s / max(t_w, 1e-6))))], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(k, op=dist.ReduceOp.MIN)
+        steps = int(k[0])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     finish()
     torch.cuda.synchronize(dev)
@@ -246,11 +312,15 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
 
-    # Roofline timing: with frames in flight a launch's start-to-end time
-    # includes the CUs it shares with its neighbours, so the kernel time of one
-    # launch is measured on its own: this rank's share, one launch after
-    # another on one stream, HIP events on that stream (rocprofv3 of
-    # `bench.py --frames-in-flight 1` gives the same average: profiles/).
+    # device errors of frames the Python pipeline rendered asynchronously
+    if pipe is not None and not native:
+        for s_ in (pipe.streams or [stream]):
+            st_, px_ = ds.stream_status(s_.cuda_stream)
+            _abi.check(st_, f"frame render (first erroring pixel {px_})")
+
+    # Single-stream kernel time (one launch after another, HIP events on that
+    # stream): the time ONE launch of this rank's share takes on an otherwise
+    # idle GPU (rocprofv3 of `--frames-in-flight 1` gives the same average).
     events = []
     for _ in range(max(1, args.roofline_frames)):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -288,6 +358,9 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
                 raise SystemExit(f"--verify: the {world}-rank frame differs from the 1-rank render")
     if native:
         pipe.close()
+    elif pipe is not None and pipe.streams:
+        for s_ in pipe.streams:
+            ds.release_stream(s_.cuda_stream)
     ds.close()
     if rank != 0:
         return None
@@ -303,47 +376,33 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         parallelism += f", {F} frames in flight on {F} render streams)"
     else:
         parallelism += ", frames rendered one after another on one stream)"
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = rays_per_frame * args.steps / elapsed / 1e6
+    frame_s = elapsed / steps
+    value = rays_per_frame * steps / elapsed / 1e6
     my_rays = stats.rays.primary + stats.rays.shadow + stats.rays.secondary
-    ops = my_rays * ops_per_ray
-    achieved_t = ops / (kernel_ms * 1e-3) / 1e12
-    alg_bytes = my_rows * W * 4  # framebuffer written once; scene/texture reads are cache-resident re-reads
     tex = texture_bytes(scene)
-    traffic = load_traffic(workload, world)
+    alg_bytes = H * W * 4  # the frame written once (all ranks together)
+    key = f"{workload}@{W}x{H}"
+    roof, roof_hbm = roofline(key, frame_s, world if split == world else 1, alg_bytes if split == world else
+                              my_rows * W * 4, tex)
+    if split != world:  # --share diagnostic: the PMC figures are whole-frame ones
+        roof.update({"achieved": None, "frac": None, "traffic": None, "basis": "--share diagnostic: not computed"})
+    ref_equiv = my_rays * ops_per_ray / (kernel_ms * 1e-3) / 1e12
     res = {
         "value": round(value, 3),
-        "ms_per_step": round(ms_per_step, 4),
+        "ms_per_step": round(frame_s * 1e3, 4),
+        "steps": steps,
+        "warmup": warmup,
         "kernel_ms": round(kernel_ms, 4),
         "data": src,
         "config": {"workload": label, "width": W, "height": H, "max_recursion_depth": scene.max_recursion_depth,
                    "bodies": body_counts, "lights": len(scene.lights), "tile_rows": TR,
-                   "parallelism": parallelism},
+                   "frames_in_flight": F, "parallelism": parallelism},
         "rays_per_frame": {"primary": rays[0], "shadow": rays[1], "secondary": rays[2], "total": rays_per_frame},
-        "roofline": {
-            "bound": "valu_fp64",
-            "achieved": round(achieved_t, 4),
-            "peak": FP64_PEAK_TOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved_t / FP64_PEAK_TOPS, 5),
-            "traffic": traffic,
-            "valu_busy_pmc": load_traffic(workload, world, "valu_busy") if (W, H) == (3840, 2160) else None,
-            "basis": f"reference-equivalent work: {ops_per_ray} FP64 ops per ray (16/sphere, 14/plane, 20/disk, "
-                     f"18/aabb; SURVEY.md 8d) x {my_rays} rays per launch / mean rg_render_kernel time (HIP events "
-                     f"around {max(1, args.roofline_frames)} single-stream launches after the timed region)" + (
-                         ". The sphere BVH and f32 pre-filter skip most of that work without changing any result, "
-                         "so frac > 1 measures the algorithmic saving over the brute-force scan, not hardware "
-                         "utilisation (DESIGN.md 4b)" if bvh.enabled else ""),
-        },
-        "roofline_hbm": {
-            "bound": "hbm",
-            "achieved": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 3),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(alg_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),
-            "traffic": traffic,
-            "basis": f"{alg_bytes} B framebuffer written per launch (+{tex} B of textures, L2/MALL resident)",
-        },
+        "roofline": roof,
+        "roofline_hbm": roof_hbm,
+        # the reference's brute-force work (16 FP64 ops per sphere test, 14 per plane ...)
+        # per single-stream launch: what the BVH and f32 pre-filter save, NOT a utilisation figure
+        "reference_equivalent_fp64_tops": round(ref_equiv, 3),
     }
     if bvh.enabled:
         res["bvh"] = {"nodes": bvh.nodes, "leaves": bvh.leaves, "depth": bvh.depth,
@@ -356,17 +415,84 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     return res
 
 
+def host_visible(workload: str, args, dev, W: int = 3840, H: int = 2160, budget_s: float = 2.0):
+    """The drop-in itself: rg_render_image (rendering.rs:24-38) returns the frame
+    in HOST memory -- render in row bands, each band's copy over PCIe overlapped
+    with the next bands' renders.  Timed back to back into a page-locked buffer
+    (rg_host_register: the DMA lands in it directly) and into a pageable one
+    (pinned staging + host memcpy)."""
+    import numpy as np
+    import torch
+
+    from raingun_amd import _abi
+    from raingun_amd.scene import DeviceScene
+
+    scene, label, _, _, _ = load_workload(workload, W, H)
+    ds = DeviceScene(scene, device=dev.index or 0)
+    st = _abi.rg_stats()
+    ref = ds.render_image(W, H, stats=st)
+    rays = st.rays.primary + st.rays.shadow + st.rays.secondary
+    res = {"workload": label, "basis": "rg_render_image back to back: frame in host memory when each call returns "
+                                       "(PCIe included; scene already in HBM)"}
+    for kind in ("pinned", "pageable"):
+        buf = np.empty((H, W, 4), dtype=np.uint8)
+        reg = _abi.HostRegistration(buf) if kind == "pinned" else None
+        try:
+            for _ in range(3):
+                ds.render_image(W, H, out=buf)
+            n, t0 = 0, time.perf_counter()
+            while n < 5 or (time.perf_counter() - t0 < budget_s and n < args.steps):
+                ds.render_image(W, H, out=buf)
+                n += 1
+            dt = (time.perf_counter() - t0) / n
+            if not np.array_equal(buf, ref):
+                raise SystemExit("host_visible: frame differs from the first render")
+        finally:
+            if reg is not None:
+                reg.close()
+        res[kind] = {"value": round(rays / dt / 1e6, 3), "ms_per_step": round(dt * 1e3, 4), "frames": n,
+                     "frame_bytes": H * W * 4, "host_GBps": round(H * W * 4 / dt / 1e9, 2)}
+    ds.close()
+    torch.cuda.synchronize(dev)
+    res["value"] = res["pinned"]["value"]
+    res["ms_per_step"] = res["pinned"]["ms_per_step"]
+    res["unit"] = "Mrays/s"
+    return res
+
+
+# Extra line items: (key, workload, size, CPU baseline?) -- BASELINE configs[2..4] and the north_star scene.
+EXTRA_LINES = [
+    ("test3_4k", "test3", (3840, 2160), True),                         # configs[2]
+    ("north_star_1024_spheres", "synth1024", (3840, 2160), True),      # north_star: 1024 spheres, 4K, depth 5
+    ("north_star_1024_spheres_8k", "synth1024", (7680, 4320), False),  # configs[3] (CPU rate: the 4K line's scene)
+    ("synth4096_16k", "synth4096p8d8", (16384, 16384), True),          # configs[4]
+]
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node (one process each).  Outside a launcher, N > 1 starts "
+                         "torch.distributed.run with N ranks itself; inside one it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="test1", help="test1 | test3 | synth<N>")
+    ap.add_argument("--workload", default="test1", help="test1 | test3 | synth<N>[p<planes>][d<depth>]")
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-north-star", action="store_true",
-                    help="skip the extra north_star line items (1024 spheres, depth 5, 3840x2160 and 7680x4320)")
+    ap.add_argument("--no-north-star", "--no-extra", dest="no_extra", action="store_true",
+                    help="skip the extra line items (configs[2..4], the north_star scene, host_visible)")
+    ap.add_argument("--extra", default="",
+                    help="comma-separated subset of the extra lines to run (test3_4k, north_star_1024_spheres, "
+                         "north_star_1024_spheres_8k, synth4096_16k, host_visible); default all")
+    ap.add_argument("--extra-budget", type=float, default=3.0,
+                    help="seconds of timed frames per extra line (at least 3 frames, at most --steps)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo: rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank renders on GPU 0 (use with --backend gloo)")
@@ -376,7 +502,7 @@ def main() -> None:
     ap.add_argument("--one-render-stream", action="store_true",
                     help="render every frame on one stream (N>1: only the gathers overlap the renders)")
     ap.add_argument("--roofline-frames", type=int, default=10,
-                    help="single-stream launches timed after the timed region for the roofline's kernel time")
+                    help="single-stream launches timed after the timed region (kernel_ms)")
     ap.add_argument("--rccl-rehearsal", action="store_true",
                     help="N=1: run the N>1 path anyway (RCCL process group, per-frame gather, re-interleave)")
     ap.add_argument("--python-pipeline", action="store_true",
@@ -391,7 +517,39 @@ def main() -> None:
                     help="diagnostic at N=1: time rank 0's share of an S-way split (no gather); value counts its rays")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 checks the gathered frame against a 1-rank render, byte for byte")
+    ap.add_argument("--plan", action="store_true",
+                    help="print this rank's launch plan (rank, world, device) as JSON and exit before any GPU work")
     args = ap.parse_args()
+
+    # One process per GPU.  `--gpus N` outside a launcher: start torch.distributed.run
+    # with N ranks on this node as a CHILD process (nothing here has touched the GPU
+    # yet) and exit with its status; inside a launcher WORLD_SIZE must agree.
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()),
+               *sys.argv[1:]]
+        sys.exit(subprocess.call(cmd))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU "
+                         f"(torchrun --nproc-per-node {args.gpus}) or drop --gpus")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:
+        local_rank = 0
+    if args.plan:
+        line = {"rank": rank, "world": world, "local_rank": local_rank, "n_gpus": world}
+        if args.backend == "gloo" and world > 1:  # rehearse the rendezvous without a GPU
+            import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+            dist.barrier()
+            dist.destroy_process_group()
+        print(json.dumps(line), flush=True)
+        return
+
     # the JSON line is the only thing on stdout: library banners (RCCL prints its
     # version block on stdout when a communicator is created) go to stderr
     json_out = os.fdopen(os.dup(1), "w")
@@ -407,11 +565,6 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.same_device:
-        local_rank = 0
     if world > 1 or args.rccl_rehearsal:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
@@ -428,13 +581,19 @@ def main() -> None:
     cpu = (not args.no_cpu_baseline) and world == 1
 
     main_res = measure(args.workload, args, world, rank, local_rank, dev, cpu)
-    ns_res = ns8k_res = None
-    if not args.no_north_star and args.workload != "synth1024":
-        ns_res = measure("synth1024", args, world, rank, local_rank, dev, cpu)
-    if not args.no_north_star:
-        # BASELINE configs[3]: the north-star scene at 7680x4320, row-tiled over the N GPUs
-        # (the CPU rate per ray is the 3840x2160 line's: same scene, same rays per pixel)
-        ns8k_res = measure("synth1024", args, world, rank, local_rank, dev, False, size=(7680, 4320))
+    extras = {}
+    if not args.no_extra:
+        want = set(filter(None, args.extra.split(","))) or None
+        for key, wl, size, with_cpu in EXTRA_LINES:
+            if want is not None and key not in want:
+                continue
+            if (wl, size) == (args.workload, (args.width, args.height)):
+                continue
+            warm = 2 if size[0] * size[1] >= 100_000_000 else min(args.warmup, 5)
+            extras[key] = measure(wl, args, world, rank, local_rank, dev, cpu and with_cpu, size=size,
+                                  warmup=warm, budget_s=args.extra_budget)
+        if world == 1 and (want is None or "host_visible" in want):
+            extras["host_visible"] = host_visible(args.workload, args, dev, args.width, args.height)
 
     if rank == 0:
         line = {
@@ -450,11 +609,8 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "f64",
         }
-        line.update({k: v for k, v in main_res.items() if k not in ("value", "ms_per_step")})
-        if ns_res is not None:
-            line["north_star_1024_spheres"] = ns_res
-        if ns8k_res is not None:
-            line["north_star_1024_spheres_8k"] = ns8k_res
+        line.update({k: v for k, v in main_res.items() if k not in ("value", "ms_per_step", "steps", "warmup")})
+        line.update(extras)
         print(json.dumps(line), file=json_out, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
