@@ -16,9 +16,10 @@ recursion depth 5.  Extra line items on the same N GPUs: configs[2]
 5), configs[3] (the same at 7680x4320) and configs[4] (4096 spheres + 8
 planes, 16384x16384, depth 8); at N=1 `host_visible` times the drop-in itself,
 rg_render_image, with the frame in host memory when each call returns.
-Frames are kept in flight (6, each on its own render stream): the timed
+Frames are kept in flight (8, each on its own render stream): the timed
 region holds `--steps` complete frames (fewer for the slow extra lines, see
-`steps` in each).
+`steps` in each), after `--settle-s` seconds of untimed frames and the
+`--warmup` untimed steps.
 
 Prints ONE JSON line on rank 0 (the driver's contract).  `roofline` is the
 executed-work VALU roofline: issue cycles of the instructions the kernels
@@ -219,10 +220,11 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
     slot = rd.slot_rows(H, split, TR)  # equal-size gather slots (last ranks zero-padded)
     out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
-    # frames in flight, each on its own render stream and hardware queue (12 per
-    # process, see main): 6 -- the whole frame is flat from 4 up, a 1/8 test1
-    # share gains 12 % from 4 to 6 (profiles/r01/bench_frames_in_flight_ab.txt)
-    F = args.frames_in_flight if args.frames_in_flight > 0 else 6
+    # frames in flight, each on its own render stream and hardware queue (16 per
+    # process, see main): 8 -- the whole frame is flat from 4 up; a rank's 1/8
+    # share of the north-star frame renders in 0.481 / 0.461 / 0.439 / 0.441 ms
+    # at 4 / 6 / 8 / 10 (profiles/r02/share_sweep.txt)
+    F = args.frames_in_flight if args.frames_in_flight > 0 else 8
     if W * H >= 100_000_000:
         F = min(F, 3)  # 1 GB frames (configs[4]): three in flight fill the GPU as well
     use_pipe = args.backend == "nccl" or world == 1
@@ -286,6 +288,19 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         dist.all_reduce(rays)
     rays = [int(x) for x in rays.tolist()]
     rays_per_frame = sum(rays)
+
+    # Settle: untimed frames for args.settle_s of wall time before the warm-up
+    # steps.  A GPU idle until now runs its first frames slowly (test1 at 20 timed
+    # steps: 0.416 ms per frame after 5 warm-up frames, 0.365 after 500;
+    # profiles/r02/settle.txt) -- the timed steps measure the steady state.
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < args.settle_s:
+        for _ in range(F):
+            step()
+        finish()
+        torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
 
     t_w = time.perf_counter()
     for _ in range(warmup):
@@ -394,6 +409,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         "warmup": warmup,
         "kernel_ms": round(kernel_ms, 4),
         "data": src,
+        "settle_s": args.settle_s,
         "config": {"workload": label, "width": W, "height": H, "max_recursion_depth": scene.max_recursion_depth,
                    "bodies": body_counts, "lights": len(scene.lights), "tile_rows": TR,
                    "frames_in_flight": F, "parallelism": parallelism},
@@ -498,9 +514,11 @@ def main() -> None:
                     help="rehearsal: every rank renders on GPU 0 (use with --backend gloo)")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames in flight, each on its own render stream (N>1: their gathers overlap later renders); "
-                         "0 = 6")
+                         "0 = 8")
     ap.add_argument("--one-render-stream", action="store_true",
                     help="render every frame on one stream (N>1: only the gathers overlap the renders)")
+    ap.add_argument("--settle-s", type=float, default=0.3,
+                    help="seconds of untimed frames before the warm-up steps (steady GPU clocks)")
     ap.add_argument("--roofline-frames", type=int, default=10,
                     help="single-stream launches timed after the timed region (kernel_ms)")
     ap.add_argument("--rccl-rehearsal", action="store_true",
@@ -556,9 +574,9 @@ def main() -> None:
     # frames in flight need a hardware queue per render stream next to RCCL's
     # stream and rank 0's re-interleave stream (HIP's default is 4 per process)
     # (the GPU box exports HIP's default, 4, so raise it rather than default it)
-    # 6 render streams + RCCL's + the communication and side streams + the null stream
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 12:
-        os.environ["GPU_MAX_HW_QUEUES"] = "12"
+    # 8 render streams + RCCL's + the communication and side streams + the null stream
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
     sys.stdout.flush()
     os.dup2(2, 1)
 

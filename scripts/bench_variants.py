@@ -2,7 +2,7 @@
 """A/B kernel variants in interleaved rounds (one subprocess per variant per round).
 
 usage: python scripts/bench_variants.py [--rounds R] [--frames K] [--workloads test1,synth1024] v1 v2 ...
-Each variant is build/variants/<name>/libraingun_hip.so.  Every run first checks
+Each variant is abvar/<name>/libraingun_hip.so.  Every run first checks
 the variant bit-exactly against the CPU restatement on small frames.
 """
 import argparse, json, os, subprocess, sys, time

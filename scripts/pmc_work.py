@@ -47,13 +47,14 @@ def counters(tagdir):
     return {c: v / frames[c] for c, v in tot.items() if frames.get(c)}
 
 
-def trace_union(tagdir, warmup, steps):
+def trace_union(tagdir, steps, tail=1):
     rows = [r for r in csv.DictReader(open(f"{tagdir}/trace/run_kernel_trace.csv")) if "rg_" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     render = [r for r in rows if "rg_render_kernel" in r["Kernel_Name"]]
-    # bench order: 1 counted render, `warmup` frames, `steps` timed frames, then single-stream launches
-    timed = render[1 + warmup:1 + warmup + steps]
-    lo_id = int(render[warmup]["Dispatch_Id"]) + 1  # first kernel after the last warm-up render
+    # bench order: 1 counted render, settle frames, warm-up frames, `steps` timed frames, then
+    # `tail` single-stream launches (--roofline-frames, 1 in scripts/pmc_work.sh)
+    timed = render[len(render) - tail - steps:len(render) - tail]
+    lo_id = int(render[len(render) - tail - steps - 1]["Dispatch_Id"]) + 1  # after the last untimed frame
     hi_id = int(timed[-1]["Dispatch_Id"])
     ivs = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
                  if lo_id <= int(r["Dispatch_Id"]) <= hi_id)
@@ -101,13 +102,13 @@ def main():
         bj = tagdir / "trace.json"
         b = json.loads(bj.read_text().strip().splitlines()[-1]) if bj.exists() and bj.read_text().strip() else {}
         try:
-            d["trace"] = trace_union(tagdir, b.get("warmup", 2), b.get("steps", steps))
+            d["trace"] = trace_union(tagdir, b.get("steps", steps))
         except Exception as e:  # noqa: BLE001
             d["trace"] = {"error": str(e)}
         if b:
             d["bench_ms_per_step_under_trace"] = b["ms_per_step"]
             d["bench_kernel_ms_single_stream"] = b.get("kernel_ms")
-        d["source"] = f"profiles/{rnd}/pmcw/{tag}.json (scripts/pmc_work.sh: rocprofv3 --pmc, 6 frames in flight)"
+        d["source"] = f"profiles/{rnd}/pmcw/{tag}.json (scripts/pmc_work.sh: rocprofv3 --pmc, the bench's frames in flight)"
         dst = REPO / "profiles" / rnd / "pmcw"
         dst.mkdir(parents=True, exist_ok=True)
         (dst / f"{tag}.json").write_text(json.dumps(d, indent=1) + "\n")

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Executed-work profile of one bench line AT ITS TIMED CONFIGURATION (6 frames in
-# flight): a kernel-trace --stats pass (per-launch durations; their per-frame
+# Executed-work profile of one bench line AT ITS TIMED CONFIGURATION (the bench's
+# frames in flight): a kernel-trace --stats pass (per-launch durations; their per-frame
 # union is compared with bench.py's ms_per_step by scripts/pmc_work.py) and
 # --pmc passes (instruction mix, HBM bytes).  Each pass is its own run, counters
 # within one block's limits, nothing but --kernel-trace beside --pmc.
