@@ -565,7 +565,7 @@ def main() -> None:
             dist.init_process_group("gloo")
             dist.barrier()
             dist.destroy_process_group()
-        print(json.dumps(line), flush=True)
+        os.write(1, (json.dumps(line) + "\n").encode())  # one write: the ranks share stdout
         return
 
     # the JSON line is the only thing on stdout: library banners (RCCL prints its

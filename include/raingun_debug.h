@@ -46,11 +46,20 @@ rg_status rg_debug_set_lane_depth(rg_scene *scene, int32_t min_depth);
  * path only.  Results are identical either way. */
 rg_status rg_debug_set_tile_order(rg_scene *scene, int32_t mode);
 
-/* Host-visible frames (rg_render_image / rg_render_tiles with a whole-frame
- * tiling): render in this many row bands, each band's device-to-host copy
- * overlapping the next bands' renders (1..16; 0 = by frame size, ~2 Mpx per
- * band, at most 4).  Results are identical for every value. */
+/* Host-visible frames (rg_render_image / rg_render_tiles without f32 RGB):
+ * -1 = ONE launch whose pixel stores go over PCIe straight into page-locked
+ * host memory (the caller's, or a pinned frame copied band by band into a
+ * pageable caller buffer as the kernel publishes finished tiles);
+ * 1..16 = render in this many row bands into device memory, each band's
+ * device-to-host copy overlapping the next bands' renders; 0 (default) =
+ * one launch for heavy-path scenes into page-locked buffers, else bands
+ * (~2 Mpx each, at most 3).  Results are identical for every value. */
 rg_status rg_debug_set_image_bands(rg_scene *scene, int32_t bands);
+
+/* Tile shape of the one-launch host-visible path: log2 of the tile width,
+ * 3 (8x8, default) .. 6 (64x1), every tile 64 pixels; wider tiles give whole
+ * row segments per PCIe write.  Device-resident renders always use 8x8. */
+rg_status rg_debug_set_host_tile_shape(rg_scene *scene, int32_t tile_wlog);
 
 /* Copy the scene's 16 statistics words after the last render: [0..2] ray
  * counts, [4..8] BVH traversal statistics when the library was built with

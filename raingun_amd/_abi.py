@@ -137,7 +137,8 @@ EXPORTED_SYMBOLS = (
 )
 # include/raingun_debug.h
 DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
-                 "rg_debug_set_tile_order", "rg_debug_set_lane_depth", "rg_debug_set_image_bands")
+                 "rg_debug_set_tile_order", "rg_debug_set_lane_depth", "rg_debug_set_image_bands",
+                 "rg_debug_set_host_tile_shape")
 # include/raingun_frames.h
 FRAMES_SYMBOLS = ("rg_frames_create", "rg_frames_destroy", "rg_frames_step", "rg_frames_flush", "rg_frames_image",
                   "rg_frames_read_image", "rg_frames_status")
@@ -193,6 +194,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_set_lane_depth.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_set_image_bands.restype = C.c_int32
     lib.rg_debug_set_image_bands.argtypes = [C.c_void_p, C.c_int32]
+    lib.rg_debug_set_host_tile_shape.restype = C.c_int32
+    lib.rg_debug_set_host_tile_shape.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_counters.restype = C.c_int32
     lib.rg_debug_counters.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.rg_frames_create.restype = C.c_int32

@@ -8,12 +8,16 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/raingun.h"
@@ -115,6 +119,9 @@ void release_image_res(rg_image_res &r) {
     if (r.d_rgba) (void)hipFree(r.d_rgba);
     if (r.d_rgb) (void)hipFree(r.d_rgb);
     if (r.h_stage) (void)hipHostFree(r.h_stage);
+    if (r.h_frame) (void)hipHostFree(r.h_frame);
+    if (r.h_flags) (void)hipHostFree(r.h_flags);
+    if (r.h_cancel) (void)hipHostFree(r.h_cancel);
     if (r.h_snap) (void)hipHostFree(r.h_snap);
     r = rg_image_res{};
 }
@@ -236,12 +243,15 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
     a.def[2] = s->def[2];
     a.max_depth = s->max_depth;
     a.fov_adjustment = fov_adjustment(s->fov);
+    a.tile_wlog = 3;  // 8x8 tiles
     return a;
 }
 
 rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
                           uint8_t *rgba_dev, float *rgb_dev, hipStream_t st, unsigned long long *snap,
-                          rg_launch_ctx **ctx_out, bool timed) {
+                          rg_launch_ctx **ctx_out, bool timed, uint32_t *tile_flags, uint32_t frame_seq,
+                          const uint32_t *cancel, uint32_t tile_wlog) {
+    if (tile_wlog < 3 || tile_wlog > 6) return RG_ERR_INVALID_ARGUMENT;
     if (!s || !rgba_dev || width == 0 || height == 0 || !tiling_valid(tiling)) return RG_ERR_INVALID_ARGUMENT;
     if (width < height) return RG_ERR_PORTRAIT;  // ray.rs:42
     const uint32_t out_rows = rg_tiling_rows(height, tiling);
@@ -264,6 +274,10 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     a.aspect = (double)width / (double)height;
     a.rgba = reinterpret_cast<uint32_t *>(rgba_dev);
     a.rgb = rgb_dev;
+    a.tile_flags = tile_flags;
+    a.frame_seq = frame_seq;
+    a.cancel = cancel;
+    a.tile_wlog = tile_wlog;
     const int frames = frames_needed(s->max_depth);
     if (frames > rg_max_array_frames() && out_rows > 0) {
         // deep recursion: frames in a global buffer sized for this launch's (persistent) grid
@@ -284,7 +298,7 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     if (!ok(hipMemsetAsync(cx->counters, 0, RG_COUNTER_WORDS * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
     if (timed && !ok(hipEventRecord(cx->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
     if (s->tile_order == 1 || (s->tile_order < 0 && rg_heavy_path(a))) {
-        const size_t ntiles = (size_t)((width + 7u) / 8u) * ((out_rows + 7u) / 8u);
+        const size_t ntiles = (size_t)rg_tile_count(a);
         if (ntiles > cx->tile_cap) {
             if (cx->tile_cost) (void)hipFree(cx->tile_cost);
             if (cx->tile_perm) (void)hipFree(cx->tile_perm);
@@ -315,6 +329,22 @@ rg_status rg_snap_status(const unsigned long long *snap, rg_stats *stats) {
         stats->error_pixel = -1;
     }
     return decode_error(snap[3], stats ? &stats->error_pixel : nullptr);
+}
+
+void *rg_host_device_ptr(void *p, size_t bytes) {
+    if (!p || bytes == 0) return nullptr;
+    auto dev = [](void *q) -> char * {
+        hipPointerAttribute_t at;
+        std::memset(&at, 0, sizeof at);
+        if (hipPointerGetAttributes(&at, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        return at.type == hipMemoryTypeHost ? static_cast<char *>(at.devicePointer) : nullptr;
+    };
+    char *d0 = dev(p), *d1 = dev(static_cast<char *>(p) + bytes - 1);
+    // one mapping: the last byte's device address continues the first's
+    return (d0 && d1 && d1 == d0 + (bytes - 1)) ? d0 : nullptr;
 }
 
 bool rg_host_is_pinned(const void *p, size_t bytes) {
@@ -687,12 +717,108 @@ rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t heig
 // one is fed from a ring of pinned staging slots by host memcpy, overlapped
 // with the following bands' DMA.  Device framebuffer, staging, streams and
 // events belong to the scene and are reused across calls.
+struct rg_copy_pool::Impl {
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv;
+    std::atomic<bool> stop{false}, active{false};
+    std::atomic<uint64_t> gen{0};
+    std::atomic<int> remaining{0};
+    unsigned char *dst = nullptr;
+    const unsigned char *src = nullptr;
+    size_t bytes = 0;
+    int parts = 1;
+};
+
+rg_copy_pool::rg_copy_pool(int helpers) : p_(new Impl) {
+    p_->parts = helpers + 1;
+    for (int i = 0; i < helpers; ++i) p_->th.emplace_back([this, i] { run(i + 1); });
+}
+
+rg_copy_pool::~rg_copy_pool() {
+    {
+        std::lock_guard<std::mutex> g(p_->m);
+        p_->stop.store(true);
+    }
+    p_->cv.notify_all();
+    for (std::thread &t : p_->th) t.join();
+    delete p_;
+}
+
+void rg_copy_pool::begin() {
+    {
+        std::lock_guard<std::mutex> g(p_->m);
+        p_->active.store(true);
+    }
+    p_->cv.notify_all();
+}
+
+void rg_copy_pool::end() { p_->active.store(false); }
+
+namespace {
+// Piece i of n of [0, bytes), 4 KiB aligned (the last piece takes the rest).
+inline void piece(size_t bytes, int i, int n, size_t &off, size_t &len) {
+    const size_t per = (bytes / (size_t)n + 4095) & ~(size_t)4095;
+    off = std::min(bytes, per * (size_t)i);
+    len = i == n - 1 ? bytes - off : std::min(bytes - off, per);
+}
+}  // namespace
+
+void rg_copy_pool::run(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+        uint64_t g = p_->gen.load(std::memory_order_acquire);
+        if (g == seen) {
+            if (p_->stop.load()) return;
+            if (p_->active.load(std::memory_order_relaxed)) {
+                __builtin_ia32_pause();
+                continue;
+            }
+            std::unique_lock<std::mutex> lk(p_->m);
+            p_->cv.wait(lk, [&] {
+                return p_->stop.load() || p_->active.load() || p_->gen.load(std::memory_order_acquire) != seen;
+            });
+            continue;
+        }
+        seen = g;
+        size_t off, len;
+        piece(p_->bytes, id, p_->parts, off, len);
+        if (len) std::memcpy(p_->dst + off, p_->src + off, len);
+        p_->remaining.fetch_sub(1, std::memory_order_acq_rel);
+    }
+}
+
+void rg_copy_pool::copy(void *dst, const void *src, size_t bytes) {
+    if (p_->parts == 1 || bytes < (256u << 10)) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    p_->dst = static_cast<unsigned char *>(dst);
+    p_->src = static_cast<const unsigned char *>(src);
+    p_->bytes = bytes;
+    p_->remaining.store(p_->parts - 1, std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> g(p_->m);  // a sleeping helper sees the new generation
+        p_->gen.fetch_add(1, std::memory_order_release);
+    }
+    p_->cv.notify_all();
+    size_t off, len;
+    piece(bytes, 0, p_->parts, off, len);
+    if (len) std::memcpy(p_->dst + off, p_->src + off, len);
+    while (p_->remaining.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+}
+
 namespace {
 
+// Bands of a banded host-visible frame: the first band's copy starts while
+// the later bands render (the frame's PCIe transfer alone: ~0.59 ms for 33 MB
+// at the measured 56 GB/s, profiles/r02/host_visible/d2h_probe.jsonl).  ~2 Mpx
+// per band, at most 3: a 4K frame in 3 bands 0.95 ms, in 16 bands 1.46 ms --
+// small launches leave most of the GPU idle (hv_sweep_bands_before.jsonl).
 int image_bands(const rg_scene *s, size_t px) {
     if (s->image_bands > 0) return s->image_bands;
-    const size_t k = px / (2u << 20);  // ~2 Mpx per band
-    return (int)std::max<size_t>(1, std::min<size_t>(RG_IMAGE_STAGE_SLOTS + 1, k));
+    const size_t k = px / RG_IMAGE_BAND_PX;
+    return (int)std::max<size_t>(1, std::min<size_t>(3, k));
 }
 
 rg_status ensure_image_res(const rg_scene *s) {
@@ -728,6 +854,108 @@ rg_status grow_device(P *&p, size_t &cap, size_t bytes) {
     return RG_OK;
 }
 
+// Pinned, coherent host buffer of at least `bytes` (grown, never shrunk).
+template <class P>
+rg_status grow_pinned(P *&p, size_t &cap, size_t bytes) {
+    if (bytes <= cap) return RG_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    void *q = nullptr;
+    if (!ok(hipHostMalloc(&q, bytes, hipHostMallocCoherent))) { (void)hipGetLastError(); return RG_ERR_OUT_OF_MEMORY; }
+    std::memset(q, 0, bytes);
+    p = static_cast<P *>(q);
+    cap = bytes;
+    return RG_OK;
+}
+
+// Wait until tiles [t0, t1) of the launch carry `seq` (the kernel publishes a
+// tile after a system-scope release of its pixels).  Polls the launch's done
+// event now and then, so a failed launch returns instead of spinning.
+rg_status wait_tiles(const uint32_t *flags, size_t t0, size_t t1, uint32_t seq, hipEvent_t done) {
+    unsigned spins = 0;
+    for (size_t i = t0; i < t1; ++i) {
+        while (__atomic_load_n(&flags[i], __ATOMIC_ACQUIRE) != seq) {
+            if ((++spins & 1023u) == 0u) {
+                const hipError_t e = hipEventQuery(done);
+                if (e == hipSuccess) {  // the kernel is done: the flag must be there now
+                    if (__atomic_load_n(&flags[i], __ATOMIC_ACQUIRE) != seq) return RG_ERR_DEVICE;
+                } else if (e != hipErrorNotReady) {
+                    (void)hipGetLastError();
+                    return RG_ERR_DEVICE;
+                }
+            }
+            __builtin_ia32_pause();
+        }
+    }
+    return RG_OK;
+}
+
+// Host-visible frame in ONE launch, no device framebuffer and no copy engine:
+// the kernel's pixel stores go straight over PCIe into page-locked host memory
+// (8x8-tile-shaped 4-B stores reach 52.7 GB/s of the 55.8 GB/s a DMA copy
+// does: profiles/r02/host_visible/d2h_probe.jsonl), so the transfer overlaps the whole
+// render.  A pinned caller buffer is written directly.  A pageable one
+// (a Rust Vec, a numpy array) is fed from a pinned frame the kernel writes:
+// the kernel publishes each finished 8x8 tile (RgKernelArgs::tile_flags) and
+// the host copies every band of rows, on RG_COPY_HELPERS + 1 threads, as
+// soon as its tiles are in, while the kernel renders the rest.
+rg_status render_host_direct(const rg_scene *s, uint32_t W, uint32_t H, const rg_tiling *t, uint32_t rows,
+                             uint8_t *rgba_out, rg_stats *stats) {
+    rg_image_res &r = s->img;
+    const size_t row4 = (size_t)W * 4, bytes = (size_t)rows * row4;
+    hipStream_t rs = r.rs[0];
+    void *dst = rg_host_device_ptr(rgba_out, std::max<size_t>(bytes, 1));
+    const bool pageable = dst == nullptr;
+    const uint32_t wl = (uint32_t)s->host_tile_wlog, TH = 64u >> wl;
+    const size_t tiles_x = ((size_t)W + (1u << wl) - 1u) >> wl, tile_rows = (rows + TH - 1u) / TH,
+                 ntiles = tiles_x * tile_rows;
+    rg_status st = RG_OK;
+    uint32_t seq = 0;
+    if (pageable) {
+        if ((st = grow_pinned(r.h_frame, r.h_frame_cap, bytes + 4)) != RG_OK) return st;
+        if ((st = grow_pinned(r.h_flags, r.h_flags_cap, (ntiles + 1) * 4)) != RG_OK) return st;
+        dst = rg_host_device_ptr(r.h_frame, std::max<size_t>(bytes, 1));
+        if (!dst) return RG_ERR_DEVICE;
+        if (++r.seq == 0) r.seq = 1;
+        seq = r.seq;
+    }
+    uint32_t *flags_dev = nullptr;
+    if (pageable && !(flags_dev = static_cast<uint32_t *>(rg_host_device_ptr(r.h_flags, ntiles * 4 + 4))))
+        return RG_ERR_DEVICE;
+    if (!ok(hipEventRecord(r.ev_t0, rs))) return RG_ERR_DEVICE;
+    st = rg_launch_tiles(s, W, H, t, static_cast<uint8_t *>(dst), nullptr, rs, r.h_snap, nullptr, false, flags_dev,
+                         seq, nullptr, wl);
+    if (st != RG_OK) return st;
+    if (!ok(hipEventRecord(r.ev_t1, rs))) return RG_ERR_DEVICE;
+    if (pageable) {
+        if (!r.pool) r.pool = std::make_shared<rg_copy_pool>(RG_COPY_HELPERS);
+        struct Active {
+            rg_copy_pool &p;
+            explicit Active(rg_copy_pool &q) : p(q) { p.begin(); }
+            ~Active() { p.end(); }
+        } active(*r.pool);
+        // bands of whole tile rows, ~RG_IMAGE_BAND_PX / 4 pixels each (the queue hands out tiles in raster order)
+        const size_t band_tr = std::max<size_t>(1, (RG_IMAGE_BAND_PX / 4) / ((size_t)W * TH));
+        for (size_t tr0 = 0; tr0 < tile_rows && st == RG_OK; tr0 += band_tr) {
+            const size_t tr1 = std::min(tile_rows, tr0 + band_tr);
+            if ((st = wait_tiles(r.h_flags, tr0 * tiles_x, tr1 * tiles_x, seq, r.ev_t1)) != RG_OK) break;
+            const size_t y0 = tr0 * TH, y1 = std::min<size_t>(rows, tr1 * TH);
+            r.pool->copy(rgba_out + y0 * row4, static_cast<uint8_t *>(r.h_frame) + y0 * row4, (y1 - y0) * row4);
+        }
+    }
+    if (!ok(hipStreamSynchronize(rs))) return RG_ERR_DEVICE;
+    if (st != RG_OK) return st;
+    rg_stats total;
+    std::memset(&total, 0, sizeof total);
+    const rg_status err = rg_snap_status(r.h_snap, &total);
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, r.ev_t0, r.ev_t1);
+    total.kernel_ms = ms;
+    if (stats) *stats = total;
+    return err;
+}
+
 }  // namespace
 
 rg_status rg_render_host(const rg_scene *s, uint32_t W, uint32_t H, const rg_tiling *t, uint8_t *rgba_out,
@@ -741,6 +969,20 @@ rg_status rg_render_host(const rg_scene *s, uint32_t W, uint32_t H, const rg_til
     rg_status st = ensure_image_res(s);
     if (st != RG_OK) return st;
     rg_image_res &r = s->img;
+    // Path choice (profiles/r02/host_visible/hv_sweep.jsonl, 4K frames): one launch writing
+    // host memory wins for trace-dominated (heavy-path) scenes into page-locked
+    // buffers (synth1024: 2.99 vs 3.63 ms banded); for shading-dominated
+    // scenes the frame's PCIe writes stall the render waves (test1: 0.95 ms
+    // either way), and into pageable memory the per-tile publication costs
+    // more than the copies it overlaps (test1 2.5 vs 1.15 ms) -- banded there.
+    if (!rgb_out) {
+        bool direct = s->image_bands < 0;
+        if (s->image_bands == 0) {
+            const RgKernelArgs pa = rg_make_args(s);
+            direct = rg_heavy_path(pa) && rg_host_device_ptr(rgba_out, std::max<size_t>((size_t)rows * W * 4, 1));
+        }
+        if (direct) return render_host_direct(s, W, H, t, rows, rgba_out, stats);
+    }
 
     // Bands.  A whole-frame tiling (stride 1) is re-cut into K bands of BR
     // rows (tiling {BR, K, b} renders exactly rows [b BR, (b+1) BR)); a sharded
@@ -816,14 +1058,22 @@ rg_status rg_render_host(const rg_scene *s, uint32_t W, uint32_t H, const rg_til
             if (!enqueue_copy(b)) return RG_ERR_DEVICE;
         if (!ok(hipStreamSynchronize(r.cs))) return RG_ERR_DEVICE;
     } else {
+        // pageable destination: DMA into the pinned staging ring, then a
+        // parallel host copy of each band while the next bands' DMA runs
+        if (!r.pool) r.pool = std::make_shared<rg_copy_pool>(RG_COPY_HELPERS);
+        struct Active {
+            rg_copy_pool &p;
+            explicit Active(rg_copy_pool &q) : p(q) { p.begin(); }
+            ~Active() { p.end(); }
+        } active(*r.pool);
         for (int b = 0; b < std::min(K, R); ++b)
             if (!enqueue_copy(b)) return RG_ERR_DEVICE;
         for (int b = 0; b < K; ++b) {
             if (!ok(hipEventSynchronize(r.ev_copy[b]))) return RG_ERR_DEVICE;
             const size_t off = banded ? (size_t)b * BR : 0;
             const uint32_t n = host_rows(b);
-            std::memcpy(rgba_out + off * row4, stage_rgba(b), (size_t)n * row4);
-            if (want_rgb) std::memcpy(rgb_out + off * (size_t)W * 3, stage_rgb(b), (size_t)n * row12);
+            r.pool->copy(rgba_out + off * row4, stage_rgba(b), (size_t)n * row4);
+            if (want_rgb) r.pool->copy(rgb_out + off * (size_t)W * 3, stage_rgb(b), (size_t)n * row12);
             if (b + R < K && !enqueue_copy(b + R)) return RG_ERR_DEVICE;
         }
     }
@@ -884,89 +1134,67 @@ rg_status rg_host_unregister(void *ptr) {
     return RG_OK;
 }
 
-// Tile-completion streaming.  Bands of `tile_rows` rows render on the scene's
-// render stream into two device slots; each band's copy to one of two pinned
-// host slots runs on the copy stream once it is rendered.  While the
-// callback holds band b, bands b+1 and b+2 render and band b+1 is copied:
-// band b+2 reuses band b's device slot (its copy is done: the host waited for
-// it) and its copy waits for band b's callback to return (host order).
+// Tile-completion streaming (render_image_stream, rendering.rs:40-69): ONE
+// launch of the whole frame writes its pixels over PCIe into a pinned,
+// coherent host frame and publishes every finished 8x8 tile
+// (RgKernelArgs::tile_flags); the host hands band after band of `tile_rows`
+// rows to the callback, in row order, as soon as the band's tiles are in,
+// while the kernel renders the rest.  A callback returning nonzero cancels:
+// the kernel takes no further tiles (RgKernelArgs::cancel; the reference's
+// `.all` short-circuits likewise) and the call returns RG_ERR_CANCELLED once
+// the tiles in flight are done.
 rg_status rg_render_stream(const rg_scene *s, uint32_t width, uint32_t height, uint32_t tile_rows,
                            rg_tile_callback on_tile, void *user, rg_stats *stats) {
     if (!s || !on_tile || width == 0 || height == 0 || tile_rows == 0) return RG_ERR_INVALID_ARGUMENT;
     if (width < height) return RG_ERR_PORTRAIT;
+    if ((unsigned long long)height * width >= (1ull << 32)) return RG_ERR_INVALID_ARGUMENT;
     if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
     rg_status st = ensure_image_res(s);
     if (st != RG_OK) return st;
     rg_image_res &r = s->img;
-    const uint32_t nb = (height + tile_rows - 1) / tile_rows;
-    const size_t band_bytes = (size_t)tile_rows * width * 4;
-    if ((st = grow_device(r.d_rgba, r.d_rgba_cap, 2 * band_bytes + 4)) != RG_OK) return st;
-    if (2 * band_bytes > r.h_stage_cap) {
-        if (r.h_stage) (void)hipHostFree(r.h_stage);
-        r.h_stage = nullptr;
-        r.h_stage_cap = 0;
-        if (!ok(hipHostMalloc(&r.h_stage, 2 * band_bytes, hipHostMallocDefault))) {
-            (void)hipGetLastError();
-            r.h_stage = nullptr;
-            return RG_ERR_OUT_OF_MEMORY;
-        }
-        r.h_stage_cap = 2 * band_bytes;
-    }
-    uint8_t *dslot[2] = {static_cast<uint8_t *>(r.d_rgba), static_cast<uint8_t *>(r.d_rgba) + band_bytes};
-    uint8_t *hslot[2] = {static_cast<uint8_t *>(r.h_stage), static_cast<uint8_t *>(r.h_stage) + band_bytes};
-    const int E = RG_IMAGE_MAX_BANDS;  // event / snapshot ring
-    auto rows_of = [&](uint32_t b) { return (b + 1) * tile_rows <= height ? tile_rows : height - b * tile_rows; };
-    auto render = [&](uint32_t b) -> rg_status {
-        rg_tiling tb = {tile_rows, nb, b};
-        hipStream_t rs = r.rs[b & 1];
-        rg_status e = rg_launch_tiles(s, width, height, &tb, dslot[b & 1], nullptr, rs, r.h_snap + 4 * (b % E), nullptr);
-        if (e == RG_OK && !ok(hipEventRecord(r.ev_done[b % E], rs))) e = RG_ERR_DEVICE;
-        return e;
-    };
-    auto copy = [&](uint32_t b) -> rg_status {
-        if (!ok(hipStreamWaitEvent(r.cs, r.ev_done[b % E], 0)) ||
-            !ok(hipMemcpyAsync(hslot[b & 1], dslot[b & 1], (size_t)rows_of(b) * width * 4, hipMemcpyDeviceToHost, r.cs)) ||
-            !ok(hipEventRecord(r.ev_copy[b % E], r.cs)))
-            return RG_ERR_DEVICE;
-        return RG_OK;
-    };
-    rg_ray_counts total = {0, 0, 0};
-    int32_t err_pixel = -1;
-    rg_status err_status = RG_OK;
-    if (!ok(hipEventRecord(r.ev_t0, r.rs[0])) || !ok(hipStreamWaitEvent(r.rs[1], r.ev_t0, 0))) st = RG_ERR_DEVICE;
-    for (uint32_t b = 0; st == RG_OK && b < std::min<uint32_t>(nb, 2); ++b) {
-        st = render(b);
-        if (st == RG_OK) st = copy(b);
-    }
-    for (uint32_t b = 0; st == RG_OK && b < nb; ++b) {
-        if (!ok(hipEventSynchronize(r.ev_copy[b % E]))) { st = RG_ERR_DEVICE; break; }
-        rg_stats bs;
-        const rg_status e = rg_snap_status(r.h_snap + 4 * (b % E), &bs);
-        total.primary += bs.rays.primary;
-        total.shadow += bs.rays.shadow;
-        total.secondary += bs.rays.secondary;
-        if (e != RG_OK && err_status == RG_OK) { err_status = e; err_pixel = bs.error_pixel; }
-        if (b + 2 < nb && (st = render(b + 2)) != RG_OK) break;  // into band b's device slot (copied)
-        if (on_tile(b * tile_rows, rows_of(b), width, hslot[b & 1], user) != 0) {
+    const size_t row4 = (size_t)width * 4, bytes = (size_t)height * row4;
+    const uint32_t wl = (uint32_t)s->host_tile_wlog, TH = 64u >> wl;
+    const size_t tiles_x = ((size_t)width + (1u << wl) - 1u) >> wl, ntiles = tiles_x * ((height + TH - 1u) / TH);
+    size_t cancel_cap = r.h_cancel ? 64 : 0;
+    if ((st = grow_pinned(r.h_frame, r.h_frame_cap, bytes + 4)) != RG_OK ||
+        (st = grow_pinned(r.h_flags, r.h_flags_cap, (ntiles + 1) * 4)) != RG_OK ||
+        (st = grow_pinned(r.h_cancel, cancel_cap, 64)) != RG_OK)
+        return st;
+    void *frame_dev = rg_host_device_ptr(r.h_frame, bytes);
+    uint32_t *flags_dev = static_cast<uint32_t *>(rg_host_device_ptr(r.h_flags, ntiles * 4 + 4));
+    const uint32_t *cancel_dev = static_cast<const uint32_t *>(rg_host_device_ptr(r.h_cancel, 4));
+    if (!frame_dev || !flags_dev || !cancel_dev) return RG_ERR_DEVICE;
+    __atomic_store_n(r.h_cancel, 0u, __ATOMIC_RELEASE);
+    if (++r.seq == 0) r.seq = 1;
+    const uint32_t seq = r.seq;
+    hipStream_t rs = r.rs[0];
+    const rg_tiling whole = {height, 1, 0};
+    if (!ok(hipEventRecord(r.ev_t0, rs))) return RG_ERR_DEVICE;
+    st = rg_launch_tiles(s, width, height, &whole, static_cast<uint8_t *>(frame_dev), nullptr, rs, r.h_snap, nullptr,
+                         false, flags_dev, seq, cancel_dev, wl);
+    if (st != RG_OK) return st;
+    if (!ok(hipEventRecord(r.ev_t1, rs))) return RG_ERR_DEVICE;
+    const uint8_t *frame = static_cast<const uint8_t *>(r.h_frame);
+    for (uint32_t y0 = 0; y0 < height; y0 += tile_rows) {
+        const uint32_t n = std::min(tile_rows, height - y0);
+        if ((st = wait_tiles(r.h_flags, (size_t)(y0 / TH) * tiles_x, ((size_t)(y0 + n) + TH - 1u) / TH * tiles_x, seq,
+                             r.ev_t1)) != RG_OK)
+            break;
+        if (on_tile(y0, n, width, frame + (size_t)y0 * row4, user) != 0) {
+            __atomic_store_n(r.h_cancel, 1u, __ATOMIC_RELEASE);
             st = RG_ERR_CANCELLED;
             break;
         }
-        if (b + 2 < nb) st = copy(b + 2);  // into band b's host slot, released by the callback
     }
-    (void)hipEventRecord(r.ev_join, r.rs[1]);
-    (void)hipStreamWaitEvent(r.rs[0], r.ev_join, 0);
-    (void)hipEventRecord(r.ev_t1, r.rs[0]);
-    (void)hipStreamSynchronize(r.rs[0]);
-    (void)hipStreamSynchronize(r.rs[1]);
-    (void)hipStreamSynchronize(r.cs);
-    if (stats) {
-        float ms = 0.0f;
-        (void)hipEventElapsedTime(&ms, r.ev_t0, r.ev_t1);
-        stats->rays = total;
-        stats->kernel_ms = ms;
-        stats->error_pixel = err_pixel;
-    }
-    if (st == RG_OK && err_status != RG_OK) return err_status;
+    if (!ok(hipStreamSynchronize(rs))) return RG_ERR_DEVICE;
+    rg_stats total;
+    std::memset(&total, 0, sizeof total);
+    const rg_status err = rg_snap_status(r.h_snap, &total);
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, r.ev_t0, r.ev_t1);
+    total.kernel_ms = ms;
+    if (stats) *stats = total;
+    if (st == RG_OK && err != RG_OK) return err;
     return st;
 }
 
@@ -1002,8 +1230,14 @@ rg_status rg_debug_set_tile_order(rg_scene *s, int32_t mode) {
 }
 
 rg_status rg_debug_set_image_bands(rg_scene *s, int32_t bands) {
-    if (!s || bands < 0 || bands > RG_IMAGE_MAX_BANDS) return RG_ERR_INVALID_ARGUMENT;
+    if (!s || bands < -1 || bands > RG_IMAGE_MAX_BANDS) return RG_ERR_INVALID_ARGUMENT;
     s->image_bands = bands;
+    return RG_OK;
+}
+
+rg_status rg_debug_set_host_tile_shape(rg_scene *s, int32_t tile_wlog) {
+    if (!s || tile_wlog < 3 || tile_wlog > 6) return RG_ERR_INVALID_ARGUMENT;
+    s->host_tile_wlog = tile_wlog;
     return RG_OK;
 }
 

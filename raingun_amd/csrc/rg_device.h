@@ -147,7 +147,28 @@ struct RgKernelArgs {
     uint32_t deep_stride;    // threads of the grid the buffer was sized for
     int32_t nan_scene;       // a body or light parameter is non-finite or >= 1e100: NaN distances possible
     unsigned long long *err_sticky;  // nullable: the launch context's error word that survives launches
+    // nullable: one word per 8x8 tile of the launch; when a wave has written a
+    // tile (rgba in page-locked host memory) it stores frame_seq there after a
+    // system-scope release, so the host can consume the tile's rows while the
+    // kernel renders on (host-visible frames into pageable memory, streaming)
+    uint32_t *tile_flags;
+    uint32_t frame_seq;
+    const uint32_t *cancel;  // nullable (host memory): nonzero = take no further tiles (streaming cancellation)
+    // Tile shape: 64 pixels (a lane each), 2^tile_wlog wide and 64 >> tile_wlog
+    // tall -- 3: 8x8 (default: ray coherence); 5: 32x2 and 6: 64x1 give whole
+    // 128/256-B row segments per store, which PCIe writes into host memory need
+    // (8x8 tiles finishing in scattered order: 29.6 GB/s, 32x2: 51-53, 64x1:
+    // 55-56; profiles/r02/host_visible/d2h_probe.jsonl)
+    uint32_t tile_wlog;
 };
+
+__host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }
+__host__ __device__ inline uint32_t rg_tile_h(const RgKernelArgs &a) { return 64u >> a.tile_wlog; }
+__host__ __device__ inline uint32_t rg_tiles_x(const RgKernelArgs &a) { return (a.width + rg_tile_w(a) - 1u) >> a.tile_wlog; }
+__host__ __device__ inline uint32_t rg_tiles_y(const RgKernelArgs &a) { return (a.out_rows + rg_tile_h(a) - 1u) / rg_tile_h(a); }
+__host__ __device__ inline unsigned long long rg_tile_count(const RgKernelArgs &a) {
+    return (unsigned long long)rg_tiles_x(a) * rg_tiles_y(a);
+}
 
 // sizeof(Frame) in rg_kernels.hip (the deep frame buffer is sized on the host)
 #define RG_FRAME_BYTES 88

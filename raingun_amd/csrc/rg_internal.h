@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <memory>
 #include <vector>
 
@@ -27,12 +28,41 @@ struct rg_launch_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
-#define RG_IMAGE_STAGE_SLOTS 3  // pinned staging slots of the host-visible image path
+#define RG_IMAGE_STAGE_SLOTS 4  // pinned staging slots of the host-visible image path
 #define RG_IMAGE_MAX_BANDS 16   // events / counter snapshots per host-visible render or stream ring
+#define RG_IMAGE_BAND_PX (2u << 20)    // ~pixels per band of a banded host-visible frame
+#ifndef RG_HOST_TILE_WLOG
+#define RG_HOST_TILE_WLOG 3     // one-launch host-visible frames: 8x8 tiles (RgKernelArgs::tile_wlog)
+#endif
+#ifndef RG_COPY_HELPERS
+#define RG_COPY_HELPERS 3       // helper threads of the pageable host copy (plus the calling thread)
+#endif
+
+// Parallel host memcpy for frames delivered into PAGEABLE caller memory: one
+// thread moves a band out of pinned staging at ~10-17 GB/s, a third of what
+// PCIe delivers (~56 GB/s), so the band is split over the calling thread and
+// RG_COPY_HELPERS helpers.  Helpers spin while a render call is in progress
+// (fork/join per band in ~1 us) and sleep between calls.
+class rg_copy_pool {
+  public:
+    explicit rg_copy_pool(int helpers);
+    ~rg_copy_pool();
+    rg_copy_pool(const rg_copy_pool &) = delete;
+    rg_copy_pool &operator=(const rg_copy_pool &) = delete;
+    void begin();  // a render call starts: helpers spin
+    void end();    // ... ends: helpers sleep
+    void copy(void *dst, const void *src, size_t bytes);  // blocking, split over all threads
+
+  private:
+    void run(int id);
+    struct Impl;
+    Impl *p_;
+};
 
 // Resources of the host-visible paths (rg_render_image / rg_render_tiles /
 // rg_render_stream), owned by the scene and reused across calls.
 struct rg_image_res {
+    std::shared_ptr<rg_copy_pool> pool;      // pageable destinations (created on first use)
     hipStream_t rs[2] = {nullptr, nullptr};  // render streams (bands alternate)
     hipStream_t cs = nullptr;                // device-to-host copies
     hipEvent_t ev_done[RG_IMAGE_MAX_BANDS] = {};
@@ -44,6 +74,12 @@ struct rg_image_res {
     size_t d_rgb_cap = 0;
     void *h_stage = nullptr;  // pinned
     size_t h_stage_cap = 0;
+    void *h_frame = nullptr;  // pinned, coherent: whole frames the kernel writes over PCIe (pageable destinations)
+    size_t h_frame_cap = 0;
+    uint32_t *h_flags = nullptr;  // pinned, coherent: per-tile publication words (RgKernelArgs::tile_flags)
+    size_t h_flags_cap = 0;       // bytes
+    uint32_t seq = 0;             // frame sequence number the flags carry
+    uint32_t *h_cancel = nullptr; // pinned, coherent: streaming cancellation word (RgKernelArgs::cancel)
     unsigned long long *h_snap = nullptr;  // pinned: 4 counter words per band
 };
 
@@ -98,7 +134,8 @@ struct rg_scene {
     double bvh_rbound = 0.0, bvh_margin = 0.0, bvh_extent = 0.0;
     rg_bvh_info bvh_info{};
     int tile_order = -1;  // expensive tiles first (rg_kernels.hip "tile ordering"): -1 auto (heavy path), 0, 1
-    int image_bands = 0;  // host-visible frames: row bands per render (0: by frame size, rg_capi.hip image_bands)
+    int image_bands = 0;  // host-visible frames: 0 auto, -1 one launch writing host memory, 1..16 row bands
+    int host_tile_wlog = RG_HOST_TILE_WLOG;  // tile shape of the one-launch host-visible path
     std::shared_ptr<const rg_host_tables> host;
     mutable std::vector<rg_launch_ctx *> ctxs;  // one per stream used
     mutable rg_launch_ctx *last = nullptr;       // the context of the latest launch (rg_debug_counters)
@@ -116,7 +153,8 @@ RgKernelArgs rg_make_args(const rg_scene *s);
 // the context's ev0/ev1 around the launch (kernel_ms).
 rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
                           uint8_t *rgba_dev, float *rgb_dev, hipStream_t stream, unsigned long long *snap,
-                          rg_launch_ctx **ctx_out, bool timed = false);
+                          rg_launch_ctx **ctx_out, bool timed = false, uint32_t *tile_flags = nullptr,
+                          uint32_t frame_seq = 0, const uint32_t *cancel = nullptr, uint32_t tile_wlog = 3);
 
 // Ray counts and status of a counter snapshot (stats nullable).
 rg_status rg_snap_status(const unsigned long long *snap, rg_stats *stats);
@@ -127,6 +165,8 @@ rg_status rg_render_host(const rg_scene *s, uint32_t width, uint32_t height, con
 
 // Is [p, p + bytes) page-locked host memory the DMA engine can write directly?
 bool rg_host_is_pinned(const void *p, size_t bytes);
+// The device address of page-locked host memory [p, p + bytes) (nullptr: not pinned).
+void *rg_host_device_ptr(void *p, size_t bytes);
 
 // A copy of `src` on `device` (same tables, same settings).
 rg_status rg_scene_replica(const rg_scene *src, int32_t device, rg_scene **out);

@@ -1112,6 +1112,19 @@ __device__ __forceinline__ uint32_t out_row_to_y(const RgKernelArgs &a, uint32_t
     return y >= a.height ? 0xFFFFFFFFu : (uint32_t)y;
 }
 
+constexpr size_t RG_NO_PIXEL = ~(size_t)0;  // a lane of a tile that lies outside the output
+
+// A wave finished tile `tile`: store its pixels (one coalesced store), then,
+// for a consumer on the host (RgKernelArgs::tile_flags), make them visible
+// (system-scope release, all lanes) and publish the tile.
+__device__ __forceinline__ void flush_tile(const RgKernelArgs &a, size_t oidx, uint32_t px, uint32_t tile, int lane) {
+    if (oidx != RG_NO_PIXEL) a.rgba[oidx] = px;
+    if (a.tile_flags) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (lane == 0) __hip_atomic_store(&a.tile_flags[tile], a.frame_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
     unsigned long long v = v32;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -1254,6 +1267,9 @@ __device__ __forceinline__ void pool_release(int slot) {  // owner: slot free ag
 
 using namespace rgk;
 
+#ifndef RG_LIGHT_BLOCK_WAVES
+#define RG_LIGHT_BLOCK_WAVES 1  // light path: waves per block (blocks retire wave by wave)
+#endif
 #ifndef RG_NQ
 #define RG_NQ 8   // tile-queue heads (see the kernel's tile loop)
 #endif
@@ -1344,12 +1360,20 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     }
 
     const int lane = threadIdx.x & 63;
+    // The wave's finished pixels wait here until its whole 8x8 tile is done,
+    // then go out as ONE coalesced store per tile (flush_tile): with the frame
+    // in host memory (host-visible renders) every store is a PCIe write whose
+    // acknowledgement the wave's next vmcnt wait would otherwise sit out once
+    // per finishing lane.
+    __shared__ uint32_t tile_px[LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS][64];
+    uint32_t *my_px = &tile_px[threadIdx.x >> 6][lane];
 #ifdef RG_BVH_STATS
     if (lane < 16) rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][lane] = 0ull;
 #endif
     [[maybe_unused]] const unsigned long long t_kernel = RG_CLOCK();
-    const uint32_t tiles_x = (a.width + 7u) / 8u;
-    const uint32_t ntiles = tiles_x * ((a.out_rows + 7u) / 8u);
+    const uint32_t tiles_x = rg_tiles_x(a);
+    const uint32_t ntiles = (uint32_t)rg_tile_count(a);
+    const uint32_t twlog = a.tile_wlog, twmask = (1u << twlog) - 1u, th = rg_tile_h(a);
     const C3 def = c3(a.def[0], a.def[1], a.def[2]);
     const int max_depth = (int)a.max_depth;
     uint32_t n_prim = 0, n_shadow = 0, n_sec = 0;
@@ -1393,6 +1417,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     uint32_t pixel = 0;        // image pixel index (error reports) of the lane's pixel or task
     int task = -1;             // pool slot whose subtree this lane computes (-1: its own pixel)
     bool tiles_left = true;    // the tile queue has not been found empty
+    uint32_t my_tile = 0xFFFFFFFFu;  // the wave's current tile (published when done: a.tile_flags)
     [[maybe_unused]] uint32_t tiles_taken = 0;
     [[maybe_unused]] bool counted = false;  // this wave is counted in rg_pool.busy
 #ifdef RG_TILE_TIMES
@@ -1653,8 +1678,8 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                             }
                         }
                         if (!handed) {
-                            a.rgba[oidx] = f32_to_u8(ret.r * 255.0f) | (f32_to_u8(ret.g * 255.0f) << 8) |
-                                           (f32_to_u8(ret.b * 255.0f) << 16) | 0xFF000000u;
+                            *my_px = f32_to_u8(ret.r * 255.0f) | (f32_to_u8(ret.g * 255.0f) << 8) |
+                                     (f32_to_u8(ret.b * 255.0f) << 16) | 0xFF000000u;
 #ifndef RG_TILE_TIMES
                             if (a.rgb) { a.rgb[3 * oidx] = ret.r; a.rgb[3 * oidx + 1] = ret.g; a.rgb[3 * oidx + 2] = ret.b; }
 #endif
@@ -1717,6 +1742,11 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             }
         }
         have_result = false;
+        // every lane of the wave is done: its tile is complete (owners hold their pixels)
+        if (my_tile != 0xFFFFFFFFu && !__any(mode != MODE_DONE)) {
+            flush_tile(a, oidx, *my_px, my_tile, lane);
+            my_tile = 0xFFFFFFFFu;
+        }
         // a wave with no live lane takes the next tile
         if (tiles_left && !__any(mode != MODE_DONE)) {
 #ifdef RG_TILE_TIMES
@@ -1729,6 +1759,11 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             cur_tile = 0xFFFFFFFFu;
 #endif
             uint32_t tile = 0xFFFFFFFFu;
+            if (a.cancel) {  // streaming: the consumer stopped (rendering.rs:53-67 `.all` short-circuits)
+                uint32_t cv = 0u;
+                if (lane == 0) cv = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (__builtin_amdgcn_readfirstlane(__shfl((int)cv, 0, 64)) != 0) qtried = RG_NQ;
+            }
             while (qtried < RG_NQ) {
                 uint32_t k = 0;
                 if (lane == 0) k = atomicAdd(reinterpret_cast<unsigned int *>(&a.counters[RG_QUEUE_BASE + RG_QUEUE_STRIDE * qi]), 1u);
@@ -1756,6 +1791,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                     if (++tiles_taken >= kmax) tiles_left = false;
                 }
                 if (a.tile_perm) tile = a.tile_perm[tile];  // scheduling order only; every tile is rendered once
+                my_tile = tile;
                 const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
 #ifdef RG_TILE_TIMES
                 cur_tile = tile;
@@ -1763,13 +1799,13 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                 t_query = 0;
                 tile_iters = 0;
 #endif
-                const uint32_t x = tx * 8u + (uint32_t)(lane & 7);
-                const uint32_t orow = ty * 8u + (uint32_t)(lane >> 3);
+                const uint32_t x = (tx << twlog) + ((uint32_t)lane & twmask);
+                const uint32_t orow = ty * th + ((uint32_t)lane >> twlog);
                 bool alive = x < a.width && orow < a.out_rows;
                 const uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
-                oidx = (size_t)orow * a.width + x;
+                oidx = alive ? (size_t)orow * a.width + x : RG_NO_PIXEL;
                 if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
-                    a.rgba[oidx] = 0u;
+                    *my_px = 0u;
 #ifndef RG_TILE_TIMES
                     if (a.rgb) { a.rgb[3 * oidx] = 0.0f; a.rgb[3 * oidx + 1] = 0.0f; a.rgb[3 * oidx + 2] = 0.0f; }
 #endif
@@ -1956,6 +1992,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
 #endif
         have_result = querying || mode == MODE_WAIT;
     }
+    if (my_tile != 0xFFFFFFFFu) flush_tile(a, oidx, *my_px, my_tile, lane);
 #ifdef RG_TILE_TIMES
     if (cur_tile != 0xFFFFFFFFu && lane == 0 && a.rgb) {
         a.rgb[cur_tile] = (float)(wall_clock64() - t_tile) * 0.01f;
@@ -2040,13 +2077,14 @@ template <bool BVH>
 __global__ __launch_bounds__(256) void rg_tile_probe_kernel(RgKernelArgs a, uint32_t *bucket_of, uint32_t ntiles) {
     const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t tile = gid / RG_PROBE_SAMPLES, smp = gid % RG_PROBE_SAMPLES;
-    const uint32_t tiles_x = (a.width + 7u) / 8u;
+    const uint32_t tiles_x = rg_tiles_x(a), tw = rg_tile_w(a), th = rg_tile_h(a);
     bool alive = tile < ntiles;
     const uint32_t ty = alive ? tile / tiles_x : 0u, tx = alive ? tile - ty * tiles_x : 0u;
-    const uint32_t ox = (smp & 3u) == 0u ? 0u : (smp & 3u) == 1u ? 7u : (smp & 3u) == 2u ? 2u : 5u;
-    const uint32_t oy = smp < 4u ? ((smp & 1u) ? 7u : 0u) : ((smp & 1u) ? 5u : 2u);
-    const uint32_t x = min(tx * 8u + ox, a.width - 1u);
-    const uint32_t orow = min(ty * 8u + oy, a.out_rows - 1u);
+    // corners and inner points of an 8x8 tile, scaled to the tile's shape
+    const uint32_t ox8 = (smp & 3u) == 0u ? 0u : (smp & 3u) == 1u ? 7u : (smp & 3u) == 2u ? 2u : 5u;
+    const uint32_t oy8 = smp < 4u ? ((smp & 1u) ? 7u : 0u) : ((smp & 1u) ? 5u : 2u);
+    const uint32_t x = min(tx * tw + ox8 * (tw - 1u) / 7u, a.width - 1u);
+    const uint32_t orow = min(ty * th + oy8 * (th - 1u) / 7u, a.out_rows - 1u);
     const uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
     uint32_t w = 0u;
     if (alive && y != 0xFFFFFFFFu) {
@@ -2144,7 +2182,7 @@ extern "C" size_t rg_tile_order_scratch_words(uint32_t ntiles) {
 }
 
 extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scratch, uint32_t *perm, hipStream_t stream) {
-    const uint32_t ntiles = ((a->width + 7u) / 8u) * ((a->out_rows + 7u) / 8u);
+    const uint32_t ntiles = (uint32_t)rg_tile_count(*a);
     const uint32_t nchunks = (ntiles + RG_ORDER_CHUNK - 1u) / RG_ORDER_CHUNK;
     uint32_t *bucket_of = scratch, *chunk_hist = scratch + ntiles;
     const uint32_t lanes = ntiles * RG_PROBE_SAMPLES;
@@ -2163,9 +2201,6 @@ extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scra
 // ---------------------------------------------------------------- launchers
 // One persistent block per CU slot: grid = CUs x (blocks per CU the register
 // and LDS budgets admit), capped by the tiles the frame has.
-#ifndef RG_LIGHT_BLOCK_WAVES
-#define RG_LIGHT_BLOCK_WAVES 1  // light path: waves per block (blocks retire wave by wave)
-#endif
 #ifndef RG_DEEP_BLOCKS_PER_CU
 #define RG_DEEP_BLOCKS_PER_CU 8  // deep-stack light launches: resident one-wave blocks per CU (bounds the frame buffer)
 #endif
@@ -2219,7 +2254,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     const hipError_t oe = occupancy(reinterpret_cast<const void *>(kern), threads, lds, cus, per_cu);
     if (oe != hipSuccess) return oe;
     if (MAXD == 0 && LB > 1 && per_cu > RG_DEEP_BLOCKS_PER_CU) per_cu = RG_DEEP_BLOCKS_PER_CU;
-    const unsigned long long tiles = (unsigned long long)((a->width + 7) / 8) * ((a->out_rows + 7) / 8);
+    const unsigned long long tiles = rg_tile_count(*a);
     const unsigned long long waves = (unsigned long long)threads / 64u;
     unsigned long long blocks = (unsigned long long)cus * per_cu;
     const unsigned long long need = (tiles + waves - 1) / waves;
@@ -2250,6 +2285,7 @@ template <int MAXD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
 static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t *gt) {
     // the BVH kernels also hold the static per-wave traversal stacks
     constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u) -
+                                (uint32_t)((LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) * 64 * 4) -  // tile_px
                                 (TASKS ? (uint32_t)sizeof(TaskPool) : 0u);
     if (a->lds_total_bytes <= budget)  // whole scene (empty sphere part if n_sph == 0)
         return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS>(a, a->lds_total_bytes, stream, gt);
@@ -2270,7 +2306,7 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
     // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
     const bool heavy = rg_heavy_path(*a);
     if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream, gt);
-    const unsigned long long tiles = (unsigned long long)((a->width + 7) / 8) * ((a->out_rows + 7) / 8);
+    const unsigned long long tiles = rg_tile_count(*a);
     const bool tasks = RG_HEAVY_TASKS && tiles < RG_HEAVY_TASK_TILES;
     if (a->n_nodes > 0)
         return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, true>(a, stream, gt)

@@ -282,6 +282,10 @@ class DeviceScene:
         """Row bands of host-visible renders (0: by frame size; include/raingun_debug.h)."""
         _abi.check(_abi.lib().rg_debug_set_image_bands(self.handle, int(bands)))
 
+    def set_host_tile_shape(self, tile_wlog: int) -> None:
+        """Tile shape of one-launch host-visible renders: log2 of the tile width, 3 (8x8) .. 6 (64x1)."""
+        _abi.check(_abi.lib().rg_debug_set_host_tile_shape(self.handle, int(tile_wlog)))
+
     def bvh_info(self) -> _abi.rg_bvh_info:
         info = _abi.rg_bvh_info()
         _abi.check(_abi.lib().rg_debug_bvh_info(self.handle, C.byref(info)))

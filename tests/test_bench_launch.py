@@ -2,6 +2,7 @@
 `--gpus N` outside a launcher starts N ranks itself, inside one it must equal
 WORLD_SIZE -- never a silent one-GPU run reported as n_gpus 1."""
 import json
+import re
 import os
 import subprocess
 import sys
@@ -19,7 +20,7 @@ def _run(args, env_extra=None):
 def test_gpus_2_outside_a_launcher_runs_two_ranks():
     p = _run(["--gpus", "2", "--plan", "--backend", "gloo"])
     assert p.returncode == 0, p.stderr[-2000:]
-    plans = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    plans = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", p.stdout)]  # ranks share the pipe
     assert sorted(x["rank"] for x in plans) == [0, 1]
     assert all(x["world"] == 2 and x["n_gpus"] == 2 for x in plans)
     assert sorted(x["local_rank"] for x in plans) == [0, 1]

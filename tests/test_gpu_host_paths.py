@@ -1,7 +1,9 @@
 """The host-facing entry points of the C ABI against the CPU restatement:
-host-visible frames (rg_render_image: banded renders overlapped with their
-copies, pageable and page-locked buffers), tile streaming with real double
-buffering (rg_render_stream), the single-process multi-GPU entry
+host-visible frames (rg_render_image: by default ONE launch whose pixel stores
+go over PCIe into page-locked memory -- the caller's, or a pinned frame whose
+published tiles are copied into a pageable caller buffer band by band while
+the kernel renders on; forced banded renders with device-to-host copies),
+tile streaming from one launch (rg_render_stream), the single-process multi-GPU entry
 (rg_render_multi), recursion deeper than the compiled frame arrays, and the
 reference's panic sites as status codes (scene.rs:38 NaN distance for
 closest-hit AND shadow rays, rendering.rs:106 transmission, bodies.rs:324
@@ -36,7 +38,7 @@ def _oracle(oracle_lib, scene, w, h):
 
 
 # ---------------------------------------------------------------- host-visible frames
-@pytest.mark.parametrize("bands", [1, 2, 3, 7])
+@pytest.mark.parametrize("bands", [-1, 0, 1, 3, 7])  # -1: one launch writing host memory; 0: automatic
 @pytest.mark.parametrize("kind,w,h", [("test1", 800, 600), ("synth200", 640, 360), ("test2", 97, 61),
                                       ("test3", 33, 9)])
 @pytest.mark.parametrize("pinned", [False, True])
@@ -55,6 +57,67 @@ def test_render_image_host_visible(oracle_lib, example_scenes, kind, w, h, bands
             assert np.array_equal(got, o_rgba)
             assert st.rays.as_dict() == o_counts
             assert st.error_pixel == -1
+    finally:
+        if reg is not None:
+            reg.close()
+        ds.close()
+
+
+@pytest.mark.parametrize("wlog", [3, 4, 5, 6])
+@pytest.mark.parametrize("kind,w,h", [("test1", 321, 243), ("synth200", 200, 111), ("test3", 97, 61)])
+def test_host_tile_shapes(oracle_lib, example_scenes, kind, w, h, wlog):
+    """One-launch host-visible frames with every tile shape (8x8 .. 64x1; the
+    tile probe and ordering, partial tiles at the right and bottom edges, the
+    band bookkeeping of the pageable copy) against the CPU restatement."""
+    scene = synthetic_scene(200, 2, 5) if kind == "synth200" else example_scenes[kind]
+    o_st, o_rgba, _, o_counts, _ = _oracle(oracle_lib, scene, w, h)
+    assert o_st == 0
+    ds = DeviceScene(scene)
+    ds.set_image_bands(-1)
+    ds.set_host_tile_shape(wlog)
+    for pinned in (False, True):
+        out = np.full((h, w, 4), 7, dtype=np.uint8)
+        reg = _abi.HostRegistration(out) if pinned else None
+        try:
+            st = _abi.rg_stats()
+            ds.render_image(w, h, stats=st, out=out)
+            assert np.array_equal(out, o_rgba)
+            assert st.rays.as_dict() == o_counts
+        finally:
+            if reg is not None:
+                reg.close()
+    got = np.zeros_like(o_rgba)
+    _abi.check(ds.render_stream(w, h, lambda r, b: got.__setitem__(slice(r, r + b.shape[0]), b), 13))
+    assert np.array_equal(got, o_rgba)
+    ds.close()
+
+
+@pytest.mark.parametrize("kind,w,h", [("test1", 3840, 2160), ("synth200", 640, 360)])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_render_image_direct_many_frames(oracle_lib, example_scenes, kind, w, h, pinned):
+    """The tile-publication protocol under load: 40 back-to-back frames into
+    the same host buffer (poisoned between calls) -- test1 at 4K (light path)
+    and a 200-sphere scene small enough for the heavy path's task splitting;
+    every frame equals the CPU restatement's, byte for byte (a tile copied
+    before its pixels landed would show)."""
+    import copy
+
+    if kind == "synth200":
+        s = synthetic_scene(200, 2, 5)
+    else:
+        s = copy.copy(example_scenes["test1"])
+        s.max_recursion_depth = 5
+    o_st, ref, _, _, _ = _oracle(oracle_lib, s, w, h)
+    assert o_st == 0
+    ds = DeviceScene(s)
+    ds.set_image_bands(-1)
+    out = np.empty((h, w, 4), dtype=np.uint8)
+    reg = _abi.HostRegistration(out) if pinned else None
+    try:
+        for k in range(40):
+            out.fill(k & 0xFF)
+            ds.render_image(w, h, out=out)
+            assert np.array_equal(out, ref), k
     finally:
         if reg is not None:
             reg.close()
@@ -97,8 +160,8 @@ def test_render_tiles_rgb_host(oracle_lib, example_scenes, tile_rows, stride, of
 @pytest.mark.parametrize("tile_rows", [32, 37, 240, 1])
 def test_stream_bands_match_oracle(oracle_lib, example_scenes, tile_rows):
     """render_image_stream (rendering.rs:40-69) as tile callbacks: every band
-    equals the CPU restatement's rows; a slow callback overlaps later bands'
-    renders and copies (the bands still arrive in order, complete)."""
+    equals the CPU restatement's rows; one launch renders on while a slow
+    callback holds a band (the bands still arrive in order, complete)."""
     s = example_scenes["test1"]
     w, h = 320, 240
     o_st, o_rgba, _, o_counts, _ = _oracle(oracle_lib, s, w, h)
