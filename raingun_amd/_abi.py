@@ -194,8 +194,9 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_set_lane_depth.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_set_image_bands.restype = C.c_int32
     lib.rg_debug_set_image_bands.argtypes = [C.c_void_p, C.c_int32]
-    lib.rg_debug_set_host_tile_shape.restype = C.c_int32
-    lib.rg_debug_set_host_tile_shape.argtypes = [C.c_void_p, C.c_int32]
+    if hasattr(lib, "rg_debug_set_host_tile_shape"):  # absent from older builds A/B runs load (RAINGUN_HIP_LIB)
+        lib.rg_debug_set_host_tile_shape.restype = C.c_int32
+        lib.rg_debug_set_host_tile_shape.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_counters.restype = C.c_int32
     lib.rg_debug_counters.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.rg_frames_create.restype = C.c_int32

@@ -250,7 +250,7 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
 rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
                           uint8_t *rgba_dev, float *rgb_dev, hipStream_t st, unsigned long long *snap,
                           rg_launch_ctx **ctx_out, bool timed, uint32_t *tile_flags, uint32_t frame_seq,
-                          const uint32_t *cancel, uint32_t tile_wlog) {
+                          const uint32_t *cancel, uint32_t tile_wlog, bool host_frame) {
     if (tile_wlog < 3 || tile_wlog > 6) return RG_ERR_INVALID_ARGUMENT;
     if (!s || !rgba_dev || width == 0 || height == 0 || !tiling_valid(tiling)) return RG_ERR_INVALID_ARGUMENT;
     if (width < height) return RG_ERR_PORTRAIT;  // ray.rs:42
@@ -278,11 +278,16 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     a.frame_seq = frame_seq;
     a.cancel = cancel;
     a.tile_wlog = tile_wlog;
+    a.defer_px = host_frame ? 1u : 0u;
     const int frames = frames_needed(s->max_depth);
-    if (frames > rg_max_array_frames() && out_rows > 0) {
-        // deep recursion: frames in a global buffer sized for this launch's (persistent) grid
+    // host-frame launches run the MAXD == 0 kernels (the only ones with the
+    // host-frame features: rg_kernels.hip HOSTF), whose frames live in a
+    // global buffer like those of recursion deeper than the compiled arrays
+    const int disp = host_frame ? std::max(frames, rg_max_array_frames() + 1) : frames;
+    if (disp > rg_max_array_frames() && out_rows > 0) {
+        // frames in a global buffer sized for this launch's (persistent) grid
         size_t threads = 0;
-        if (!ok(rg_render_grid_threads(&a, frames, &threads)) || threads == 0 || threads > 0xFFFFFFFFull)
+        if (!ok(rg_render_grid_threads(&a, disp, &threads)) || threads == 0 || threads > 0xFFFFFFFFull)
             return RG_ERR_DEVICE;
         const size_t bytes = threads * (size_t)frames * RG_FRAME_BYTES;
         if (bytes > cx->deep_bytes) {
@@ -314,7 +319,7 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
             a.tile_perm = cx->tile_perm;
         }
     }
-    if (out_rows > 0 && !ok(rg_launch_render(&a, frames, st))) return RG_ERR_DEVICE;
+    if (out_rows > 0 && !ok(rg_launch_render(&a, disp, st))) return RG_ERR_DEVICE;
     if (timed && !ok(hipEventRecord(cx->ev1, st))) return RG_ERR_DEVICE;
     if (snap && !ok(hipMemcpyAsync(snap, cx->counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st)))
         return RG_ERR_DEVICE;
@@ -925,7 +930,7 @@ rg_status render_host_direct(const rg_scene *s, uint32_t W, uint32_t H, const rg
         return RG_ERR_DEVICE;
     if (!ok(hipEventRecord(r.ev_t0, rs))) return RG_ERR_DEVICE;
     st = rg_launch_tiles(s, W, H, t, static_cast<uint8_t *>(dst), nullptr, rs, r.h_snap, nullptr, false, flags_dev,
-                         seq, nullptr, wl);
+                         seq, nullptr, wl, true);
     if (st != RG_OK) return st;
     if (!ok(hipEventRecord(r.ev_t1, rs))) return RG_ERR_DEVICE;
     if (pageable) {
@@ -1171,7 +1176,7 @@ rg_status rg_render_stream(const rg_scene *s, uint32_t width, uint32_t height, u
     const rg_tiling whole = {height, 1, 0};
     if (!ok(hipEventRecord(r.ev_t0, rs))) return RG_ERR_DEVICE;
     st = rg_launch_tiles(s, width, height, &whole, static_cast<uint8_t *>(frame_dev), nullptr, rs, r.h_snap, nullptr,
-                         false, flags_dev, seq, cancel_dev, wl);
+                         false, flags_dev, seq, cancel_dev, wl, true);
     if (st != RG_OK) return st;
     if (!ok(hipEventRecord(r.ev_t1, rs))) return RG_ERR_DEVICE;
     const uint8_t *frame = static_cast<const uint8_t *>(r.h_frame);

@@ -160,6 +160,7 @@ struct RgKernelArgs {
     // (8x8 tiles finishing in scattered order: 29.6 GB/s, 32x2: 51-53, 64x1:
     // 55-56; profiles/r02/host_visible/d2h_probe.jsonl)
     uint32_t tile_wlog;
+    uint32_t defer_px;  // 1: hold pixels in LDS, one store per finished tile (the frame is in host memory)
 };
 
 __host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }

@@ -1118,7 +1118,7 @@ constexpr size_t RG_NO_PIXEL = ~(size_t)0;  // a lane of a tile that lies outsid
 // for a consumer on the host (RgKernelArgs::tile_flags), make them visible
 // (system-scope release, all lanes) and publish the tile.
 __device__ __forceinline__ void flush_tile(const RgKernelArgs &a, size_t oidx, uint32_t px, uint32_t tile, int lane) {
-    if (oidx != RG_NO_PIXEL) a.rgba[oidx] = px;
+    if (a.defer_px && oidx != RG_NO_PIXEL) a.rgba[oidx] = px;
     if (a.tile_flags) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         if (lane == 0) __hip_atomic_store(&a.tile_flags[tile], a.frame_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1360,20 +1360,26 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
     }
 
     const int lane = threadIdx.x & 63;
-    // The wave's finished pixels wait here until its whole 8x8 tile is done,
-    // then go out as ONE coalesced store per tile (flush_tile): with the frame
-    // in host memory (host-visible renders) every store is a PCIe write whose
+    // With the frame in host memory (a.defer_px) the wave's finished pixels
+    // wait here until its whole tile is done, then go out as ONE coalesced
+    // store per tile (flush_tile): every store is a PCIe write whose
     // acknowledgement the wave's next vmcnt wait would otherwise sit out once
     // per finishing lane.
-    __shared__ uint32_t tile_px[LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS][64];
-    uint32_t *my_px = &tile_px[threadIdx.x >> 6][lane];
+    // Host-frame features (deferred tile stores, tile publication, streaming
+    // cancellation, tile shapes other than 8x8) exist only in the MAXD == 0
+    // instantiations, which host-visible one-launch renders use: the array
+    // instantiations of device-resident renders stay as lean as before (the
+    // runtime checks alone cost test1 3 %, profiles/r02/ab_hostf.txt).
+    constexpr bool HOSTF = MAXD == 0;
+    __shared__ uint32_t tile_px[HOSTF ? (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) : 1][64];
+    uint32_t *my_px = &tile_px[HOSTF ? threadIdx.x >> 6 : 0][lane];
 #ifdef RG_BVH_STATS
     if (lane < 16) rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][lane] = 0ull;
 #endif
     [[maybe_unused]] const unsigned long long t_kernel = RG_CLOCK();
-    const uint32_t tiles_x = rg_tiles_x(a);
-    const uint32_t ntiles = (uint32_t)rg_tile_count(a);
-    const uint32_t twlog = a.tile_wlog, twmask = (1u << twlog) - 1u, th = rg_tile_h(a);
+    const uint32_t twlog = HOSTF ? a.tile_wlog : 3u, twmask = (1u << twlog) - 1u, th = 64u >> twlog;
+    const uint32_t tiles_x = (a.width + twmask) >> twlog;
+    const uint32_t ntiles = tiles_x * ((a.out_rows + th - 1u) / th);
     const C3 def = c3(a.def[0], a.def[1], a.def[2]);
     const int max_depth = (int)a.max_depth;
     uint32_t n_prim = 0, n_shadow = 0, n_sec = 0;
@@ -1678,8 +1684,10 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                             }
                         }
                         if (!handed) {
-                            *my_px = f32_to_u8(ret.r * 255.0f) | (f32_to_u8(ret.g * 255.0f) << 8) |
-                                     (f32_to_u8(ret.b * 255.0f) << 16) | 0xFF000000u;
+                            const uint32_t px = f32_to_u8(ret.r * 255.0f) | (f32_to_u8(ret.g * 255.0f) << 8) |
+                                                (f32_to_u8(ret.b * 255.0f) << 16) | 0xFF000000u;
+                            if (HOSTF && a.defer_px) *my_px = px;
+                            else a.rgba[oidx] = px;
 #ifndef RG_TILE_TIMES
                             if (a.rgb) { a.rgb[3 * oidx] = ret.r; a.rgb[3 * oidx + 1] = ret.g; a.rgb[3 * oidx + 2] = ret.b; }
 #endif
@@ -1743,7 +1751,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
         }
         have_result = false;
         // every lane of the wave is done: its tile is complete (owners hold their pixels)
-        if (my_tile != 0xFFFFFFFFu && !__any(mode != MODE_DONE)) {
+        if (HOSTF && my_tile != 0xFFFFFFFFu && (a.defer_px || a.tile_flags) && !__any(mode != MODE_DONE)) {
             flush_tile(a, oidx, *my_px, my_tile, lane);
             my_tile = 0xFFFFFFFFu;
         }
@@ -1759,7 +1767,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
             cur_tile = 0xFFFFFFFFu;
 #endif
             uint32_t tile = 0xFFFFFFFFu;
-            if (a.cancel) {  // streaming: the consumer stopped (rendering.rs:53-67 `.all` short-circuits)
+            if (HOSTF && a.cancel) {  // streaming: the consumer stopped (rendering.rs:53-67 `.all` short-circuits)
                 uint32_t cv = 0u;
                 if (lane == 0) cv = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (__builtin_amdgcn_readfirstlane(__shfl((int)cv, 0, 64)) != 0) qtried = RG_NQ;
@@ -1791,7 +1799,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                     if (++tiles_taken >= kmax) tiles_left = false;
                 }
                 if (a.tile_perm) tile = a.tile_perm[tile];  // scheduling order only; every tile is rendered once
-                my_tile = tile;
+                if constexpr (HOSTF) my_tile = tile;
                 const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
 #ifdef RG_TILE_TIMES
                 cur_tile = tile;
@@ -1803,9 +1811,10 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
                 const uint32_t orow = ty * th + ((uint32_t)lane >> twlog);
                 bool alive = x < a.width && orow < a.out_rows;
                 const uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
-                oidx = alive ? (size_t)orow * a.width + x : RG_NO_PIXEL;
+                oidx = (HOSTF && !alive) ? RG_NO_PIXEL : (size_t)orow * a.width + x;
                 if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
-                    *my_px = 0u;
+                    if (HOSTF && a.defer_px) *my_px = 0u;
+                    else a.rgba[oidx] = 0u;
 #ifndef RG_TILE_TIMES
                     if (a.rgb) { a.rgb[3 * oidx] = 0.0f; a.rgb[3 * oidx + 1] = 0.0f; a.rgb[3 * oidx + 2] = 0.0f; }
 #endif
@@ -1992,7 +2001,7 @@ __global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
 #endif
         have_result = querying || mode == MODE_WAIT;
     }
-    if (my_tile != 0xFFFFFFFFu) flush_tile(a, oidx, *my_px, my_tile, lane);
+    if (HOSTF && my_tile != 0xFFFFFFFFu && (a.defer_px || a.tile_flags)) flush_tile(a, oidx, *my_px, my_tile, lane);
 #ifdef RG_TILE_TIMES
     if (cur_tile != 0xFFFFFFFFu && lane == 0 && a.rgb) {
         a.rgb[cur_tile] = (float)(wall_clock64() - t_tile) * 0.01f;
@@ -2285,7 +2294,7 @@ template <int MAXD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
 static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t *gt) {
     // the BVH kernels also hold the static per-wave traversal stacks
     constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u) -
-                                (uint32_t)((LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) * 64 * 4) -  // tile_px
+                                (uint32_t)(MAXD != 0 ? 0 : (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) * 64 * 4) -  // tile_px
                                 (TASKS ? (uint32_t)sizeof(TaskPool) : 0u);
     if (a->lds_total_bytes <= budget)  // whole scene (empty sphere part if n_sph == 0)
         return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS>(a, a->lds_total_bytes, stream, gt);
