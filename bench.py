@@ -433,10 +433,12 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
 
 def host_visible(workload: str, args, dev, W: int = 3840, H: int = 2160, budget_s: float = 2.0):
     """The drop-in itself: rg_render_image (rendering.rs:24-38) returns the frame
-    in HOST memory -- render in row bands, each band's copy over PCIe overlapped
-    with the next bands' renders.  Timed back to back into a page-locked buffer
-    (rg_host_register: the DMA lands in it directly) and into a pageable one
-    (pinned staging + host memcpy)."""
+    in HOST memory.  Timed back to back into a page-locked buffer
+    (rg_host_register: heavy scenes render in one launch whose pixel stores
+    go over PCIe straight into it; others in row bands whose DMA copies land
+    in it directly while later bands render) and into a pageable one (banded,
+    pinned staging + a parallel host copy).  PCIe alone: 33 MB per 4K frame at
+    the measured 56 GB/s = 0.59 ms (profiles/r02/host_visible/d2h_probe.jsonl)."""
     import numpy as np
     import torch
 
@@ -506,7 +508,8 @@ def main() -> None:
                     help="skip the extra line items (configs[2..4], the north_star scene, host_visible)")
     ap.add_argument("--extra", default="",
                     help="comma-separated subset of the extra lines to run (test3_4k, north_star_1024_spheres, "
-                         "north_star_1024_spheres_8k, synth4096_16k, host_visible); default all")
+                         "north_star_1024_spheres_8k, synth4096_16k, host_visible, host_visible_north_star); "
+                         "default all")
     ap.add_argument("--extra-budget", type=float, default=3.0,
                     help="seconds of timed frames per extra line (at least 3 frames, at most --steps)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo: rehearsal)")
@@ -612,6 +615,8 @@ def main() -> None:
                                   warmup=warm, budget_s=args.extra_budget)
         if world == 1 and (want is None or "host_visible" in want):
             extras["host_visible"] = host_visible(args.workload, args, dev, args.width, args.height)
+        if world == 1 and (want is None or "host_visible_north_star" in want) and args.workload != "synth1024":
+            extras["host_visible_north_star"] = host_visible("synth1024", args, dev, 3840, 2160)
 
     if rank == 0:
         line = {

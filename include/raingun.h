@@ -166,10 +166,12 @@ rg_status rg_scene_set_max_depth(rg_scene *scene, uint32_t max_recursion_depth);
 /* Blocking whole-frame render into a caller-owned host buffer of
  * width*height*4 bytes (row-major RGBA8, alpha 255).
  * Replaces rendering::render_image (rendering.rs:24-38). `stats` may be NULL.
- * The frame renders in row bands whose device-to-host copies overlap the
- * later bands' renders; a pinned `rgba_out` (rg_host_register, or memory from
- * hipHostMalloc) receives the DMA directly, a pageable one through pinned
- * staging.  Any max_recursion_depth renders (scene.rs:16 is a u32): depths
+ * Into a pinned `rgba_out` (rg_host_register, or memory from hipHostMalloc)
+ * a heavy (trace-dominated) scene renders in ONE launch whose pixel stores go
+ * over PCIe straight into the buffer; otherwise the frame renders in row
+ * bands whose device-to-host copies overlap the later bands' renders (the DMA
+ * lands directly in a pinned buffer; a pageable one is filled from pinned
+ * staging by several host threads).  Any max_recursion_depth renders (scene.rs:16 is a u32): depths
  * above 65 keep their shading frames in device memory.  On a device error
  * (RG_ERR_AABB_NORMAL / _NAN_DISTANCE / _TRANSMISSION: the reference's
  * panics) the frame is still delivered and stats->error_pixel names the first
@@ -219,11 +221,13 @@ rg_status rg_render_tiles(const rg_scene *scene, uint32_t width, uint32_t height
 uint32_t rg_tiling_rows(uint32_t height, const rg_tiling *tiling);
 
 /* Tile-completion streaming (replaces render_image_stream, rendering.rs:40-69,
- * which sends one RenderedPixel per pixel over an mpsc channel): the frame is
- * rendered in bands of `tile_rows` rows; after each band `on_tile` receives the
- * band's RGBA8 rows on the host.  A non-zero return from `on_tile` cancels the
- * remaining bands (the reference's `.all` stops when the channel closes) and
- * the call returns RG_ERR_CANCELLED. */
+ * which sends one RenderedPixel per pixel over an mpsc channel): ONE launch
+ * renders the frame into page-locked host memory and publishes every finished
+ * tile; `on_tile` receives each band of `tile_rows` rows, in row order, as soon
+ * as the band is complete, while the kernel renders on.  A non-zero return
+ * from `on_tile` cancels: the kernel takes no further tiles (the reference's
+ * `.all` stops when the channel closes) and the call returns RG_ERR_CANCELLED.
+ * The band pointer is valid only during the callback. */
 typedef int32_t (*rg_tile_callback)(uint32_t row_begin, uint32_t rows, uint32_t width,
                                     const uint8_t *rgba, void *user);
 rg_status rg_render_stream(const rg_scene *scene, uint32_t width, uint32_t height,

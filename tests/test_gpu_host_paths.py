@@ -262,6 +262,42 @@ def test_nan_distance_single_hit_shadow_is_occluded(oracle_lib, path):
 
 
 @pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("w,h", [(33, 21), (65, 37)])
+def test_rays_in_aabb_slab_planes(oracle_lib, path, w, h):
+    """Rays lying exactly in a slab plane of a box (d_k == 0 and o_k on the
+    face: 0 * inf = NaN inside the slab test, bodies.rs:242-282).  The NaN
+    never reaches Scene::trace: a NaN tmin/tmax loses every comparison and the
+    test returns only tmin >= 0 or tmax >= 0, so these rays hit or miss like
+    the reference and nothing panics.  The odd width puts the middle column's
+    primary rays at d.x == 0 on the box face x = 0; their floor hits have
+    x == 0 exactly, so the shadow rays towards the overhead light (d = (0,1,0))
+    run inside the same face plane (and inside z-face planes: d.z == 0)."""
+    m = Material(WHITE, 0.5)
+    scene = Scene(bodies=[AABB(((0.0, -1.0, -5.0), (1.0, 1.0, -3.0)), m),
+                          AABB(((-2.0, -1.5, -4.0), (0.0, -1.0, -2.5)), Material(Color.from_str("#ff8040"), 0.4)),
+                          Plane((0.0, -2.0, 0.0), (0.0, -1.0, 0.0), m)],
+                  lights=[DirectionalLight((0.0, -1.0, 0.0), WHITE, 1.0),
+                          SphericalLight((0.0, 3.0, -4.0), WHITE, 300.0)])
+    assert _error_case(oracle_lib, scene, w, h, path) == _abi.RG_OK
+    # the closest-hit query itself on rays in slab planes: faces, edges, corners, both signs of zero
+    rays = []
+    for o in [(0.0, -2.0, -4.0), (0.0, 0.0, 0.0), (1.0, -1.0, -3.0), (0.0, -1.0, -5.0), (-2.0, -1.5, -2.5),
+              (0.5, 1.0, -4.0), (0.0, 0.5, -3.0)]:
+        for d in [(0.0, 1.0, 0.0), (0.0, -1.0, 0.0), (-0.0, 1.0, 0.0), (0.0, 0.0, -1.0), (0.0, 0.0, 1.0),
+                  (1.0, 0.0, 0.0), (-1.0, 0.0, -0.0), (0.6, 0.0, -0.8), (0.0, 0.6, -0.8)]:
+            rays.append([*o, *d])
+    rays = np.array(rays)
+    o_st, o_dist, o_body = oracle_lib.trace(SceneDesc(scene), rays)
+    assert o_st == 0
+    ds = DeviceScene(scene, path=path)
+    dist, body = ds.trace(rays)
+    ds.close()
+    assert np.array_equal(body, o_body)
+    hit = o_body >= 0
+    assert np.array_equal(dist[hit], o_dist[hit])
+
+
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("w,h", [(5, 3), (33, 21)])
 def test_transmission_none_while_kr_below_one(oracle_lib, path, w, h):
     """An odd width puts a primary ray at d.x == 0 exactly; it hits the +z face
