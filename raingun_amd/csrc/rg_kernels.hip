@@ -2304,7 +2304,7 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 }
 
 #ifndef RG_LIGHT_WPS
-#define RG_LIGHT_WPS 3            // light path: waves per SIMD (168 VGPRs)
+#define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
 #endif
 
 template <int MAXD>
