@@ -1305,7 +1305,11 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // tile from an atomic queue (counters[16..], sharded) and runs the per-lane
 // state machine until its 64 lanes have written their pixels.
 template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
-__global__ __launch_bounds__(256 * WPS) void rg_render_kernel(RgKernelArgs a) {
+// Light path (LB > 1): blocks of RG_LIGHT_BLOCK_WAVES waves, at least WPS waves
+// per SIMD (the second bound is waves per execution unit on AMD); heavy path:
+// one block of 4*WPS waves per CU.  Both cap the VGPRs at 512 / WPS.
+__global__ __launch_bounds__(LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS, LB > 1 ? WPS : 1)
+void rg_render_kernel(RgKernelArgs a) {
     static_assert(!BVH || 4 * WPS <= RG_BVH_MAX_WAVES, "one BVH stack per wave");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     typename std::conditional<LSPH, SphLds, SphScalar>::type src;
