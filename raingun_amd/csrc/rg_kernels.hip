@@ -1928,6 +1928,31 @@ void rg_render_kernel(RgKernelArgs a) {
             have_result = mode == MODE_WAIT;
             continue;
         }
+#ifdef RG_ITER_STATS
+        {  // SIMD use of the query iterations (diagnostic build), counters[4..11]: query
+           // iterations, their querying lanes; iterations with a ray of depth >= 1, their
+           // querying lanes, their depth >= 1 lanes; iterations with <= 16 querying lanes;
+           // iterations with shadow lanes, shadow lanes
+            const int qd = mode == MODE_CLOSEST ? qdepth : hdepth;
+            const unsigned long long all = __ballot(querying), sec = __ballot(querying && qd >= 1);
+            const unsigned long long shl = __ballot(querying && mode != MODE_CLOSEST);
+            const unsigned n = (unsigned)__builtin_popcountll(all);
+            if (lane == __builtin_ffsll((long long)__ballot(1)) - 1) {  // one atomic set per wave iteration
+                atomicAdd(&a.counters[4], 1ull);
+                atomicAdd(&a.counters[5], (unsigned long long)n);
+                if (sec) {
+                    atomicAdd(&a.counters[6], 1ull);
+                    atomicAdd(&a.counters[7], (unsigned long long)n);
+                    atomicAdd(&a.counters[8], (unsigned long long)__builtin_popcountll(sec));
+                }
+                if (n <= 16) atomicAdd(&a.counters[9], 1ull);
+                if (shl) {
+                    atomicAdd(&a.counters[10], 1ull);
+                    atomicAdd(&a.counters[11], (unsigned long long)__builtin_popcountll(shl));
+                }
+            }
+        }
+#endif
 #ifdef RG_TILE_TIMES
         ++tile_iters;
         const unsigned long long t_q0 = wall_clock64();
