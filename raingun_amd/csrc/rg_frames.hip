@@ -1,8 +1,9 @@
 // rg_frames.hip — frames in flight over N ranks (include/raingun_frames.h).
 //
 // Per frame k, slot b = k % depth:
-//   render stream b : wait done[b] -> render this rank's tiles into part[b] -> record rendered[b]
-//   comm stream     : wait rendered[b] -> ncclGather(part[b] -> gathered[b] on rank 0) -> record sent[b]
+//   render stream b : wait done[b] -> render this rank's tiles into part[b] (off the root: pack it
+//                     to RGB, 3 B per pixel) -> record rendered[b]
+//   comm stream     : wait rendered[b] -> ncclGather(packed[b] -> gathered[b] on rank 0) -> record sent[b]
 //   side stream     : (rank 0) wait sent[b] -> re-interleave gathered[b] into image[b] -> record done[b]
 // (non-root ranks: done[b] = sent[b]).  All gathers go through ONE stream, so
 // every rank issues and runs them in frame order; renders of consecutive frames
@@ -10,6 +11,7 @@
 // calls (the Python pipeline spent ~70 us per frame on rank 0).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -20,27 +22,89 @@ namespace {
 
 bool ok(hipError_t e) { return e == hipSuccess; }
 
+// The gathered parts travel as packed RGB, 3 B per pixel: alpha is always
+// 255 (color.rs rgba()), so a quarter of every gather's bytes over xGMI carried
+// no information.  Non-root ranks pack their part after the render; the root
+// re-interleaves its OWN rows straight from its RGBA part (its slot of the
+// gather is not read) and the others' from the packed slots, re-adding alpha.
+__global__ __launch_bounds__(256) void rg_pack_rgb_kernel(const uint32_t *rgba, uint8_t *rgb, size_t npx) {
+    const size_t g = (size_t)blockIdx.x * 256u + threadIdx.x;  // pixels 4g .. 4g+3
+    const size_t p0 = g * 4u;
+    if (p0 >= npx) return;
+    if (p0 + 4u <= npx) {
+        const uint4 v = reinterpret_cast<const uint4 *>(rgba)[g];
+        uint32_t *o = reinterpret_cast<uint32_t *>(rgb + p0 * 3u);  // 12 g bytes: dword aligned
+        o[0] = (v.x & 0xFFFFFFu) | (v.y << 24);
+        o[1] = ((v.y >> 8) & 0xFFFFu) | (v.z << 16);
+        o[2] = ((v.z >> 16) & 0xFFu) | ((v.w & 0xFFFFFFu) << 8);
+    } else {
+        for (size_t p = p0; p < npx; ++p) {
+            const uint32_t v = rgba[p];
+            rgb[3 * p] = (uint8_t)v;
+            rgb[3 * p + 1] = (uint8_t)(v >> 8);
+            rgb[3 * p + 2] = (uint8_t)(v >> 16);
+        }
+    }
+}
+
 // Image row y lives in tile t = y / T, dealt to rank t % world as that rank's
-// (t / world)-th tile: row (t / world) * T + y % T of its part (distributed.py assemble).
-__global__ __launch_bounds__(256) void rg_reinterleave_kernel(const uint32_t *gathered, uint32_t *image, uint32_t width,
-                                                              uint32_t height, uint32_t tile_rows, uint32_t world,
-                                                              uint32_t slot_rows) {
+// (t / world)-th tile: row (t / world) * T + y % T of its part (distributed.py
+// assemble).  Rank 0's rows come from root_part (RGBA), the others' from
+// their packed slots (slot_bytes apart).  4 pixels per thread.
+__global__ __launch_bounds__(256) void rg_reinterleave_kernel(const uint8_t *gathered, const uint32_t *root_part,
+                                                              uint32_t *image, uint32_t width, uint32_t height,
+                                                              uint32_t tile_rows, uint32_t world, size_t slot_bytes) {
     const uint32_t y = blockIdx.y;
-    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
-    if (y >= height || x >= width) return;
+    const uint32_t x0 = (blockIdx.x * 256u + threadIdx.x) * 4u;
+    if (y >= height || x0 >= width) return;
     const uint32_t t = y / tile_rows;
     const uint32_t r = t % world;
     const uint32_t src_row = (t / world) * tile_rows + (y - t * tile_rows);
-    image[(size_t)y * width + x] = gathered[((size_t)r * slot_rows + src_row) * width + x];
+    uint32_t *dst = image + (size_t)y * width + x0;
+    const size_t src_px = (size_t)src_row * width + x0;
+    if (r == 0) {
+        const uint32_t n = min(4u, width - x0);
+        for (uint32_t k = 0; k < n; ++k) dst[k] = root_part[src_px + k];
+        return;
+    }
+    const uint8_t *src = gathered + (size_t)r * slot_bytes + src_px * 3u;
+    if ((width & 3u) == 0u) {  // whole, dword-aligned groups of 4 pixels
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(src);
+        const uint32_t a = w[0], b = w[1], c = w[2];
+        uint4 o;
+        o.x = (a & 0xFFFFFFu) | 0xFF000000u;
+        o.y = (a >> 24) | ((b & 0xFFFFu) << 8) | 0xFF000000u;
+        o.z = (b >> 16) | ((c & 0xFFu) << 16) | 0xFF000000u;
+        o.w = (c >> 8) | 0xFF000000u;
+        *reinterpret_cast<uint4 *>(dst) = o;
+    } else {
+        const uint32_t n = min(4u, width - x0);
+        for (uint32_t k = 0; k < n; ++k)
+            dst[k] = (uint32_t)src[3 * k] | ((uint32_t)src[3 * k + 1] << 8) | ((uint32_t)src[3 * k + 2] << 16) |
+                     0xFF000000u;
+    }
 }
 
 }  // namespace
 
-hipError_t rg_launch_reinterleave(const void *gathered, void *image, uint32_t width, uint32_t height, uint32_t tile_rows,
-                                  uint32_t world, uint32_t slot_rows, hipStream_t stream) {
-    dim3 grid((width + 255u) / 256u, height);
-    hipLaunchKernelGGL(rg_reinterleave_kernel, grid, dim3(256), 0, stream, static_cast<const uint32_t *>(gathered),
-                       static_cast<uint32_t *>(image), width, height, tile_rows, world, slot_rows);
+size_t rg_packed_slot_bytes(uint32_t slot_rows, uint32_t width) {
+    return ((size_t)slot_rows * width * 3u + 15u) & ~(size_t)15u;
+}
+
+hipError_t rg_launch_pack_rgb(const void *rgba, void *rgb, size_t npx, hipStream_t stream) {
+    const size_t groups = (npx + 3u) / 4u;
+    hipLaunchKernelGGL(rg_pack_rgb_kernel, dim3((unsigned)((groups + 255u) / 256u)), dim3(256), 0, stream,
+                       static_cast<const uint32_t *>(rgba), static_cast<uint8_t *>(rgb), npx);
+    return hipGetLastError();
+}
+
+hipError_t rg_launch_reinterleave(const void *gathered, const void *root_part, void *image, uint32_t width,
+                                  uint32_t height, uint32_t tile_rows, uint32_t world, size_t slot_bytes,
+                                  hipStream_t stream) {
+    dim3 grid((((width + 3u) / 4u) + 255u) / 256u, height);
+    hipLaunchKernelGGL(rg_reinterleave_kernel, grid, dim3(256), 0, stream, static_cast<const uint8_t *>(gathered),
+                       static_cast<const uint32_t *>(root_part), static_cast<uint32_t *>(image), width, height,
+                       tile_rows, world, slot_bytes);
     return hipGetLastError();
 }
 
@@ -49,13 +113,14 @@ struct rg_frames {
     int device = 0;
     uint32_t w = 0, h = 0, T = 0, slot_rows = 0;
     int rank = 0, world = 1, depth = 1;
-    size_t part_bytes = 0;
+    size_t part_bytes = 0;   // RGBA part of a frame
+    size_t slot_bytes = 0;   // packed RGB part: what each rank sends (rg_packed_slot_bytes)
     rg_tiling tiling{};
     void *comm = nullptr;
     rg_gather_fn gather = nullptr;
     std::vector<hipStream_t> render;
     hipStream_t comm_stream = nullptr, side = nullptr;
-    std::vector<void *> parts, gathered, image;
+    std::vector<void *> parts, packed, gathered, image;
     std::vector<hipEvent_t> rendered, sent, done;
     unsigned long long k = 0;
     int last = -1;
@@ -72,6 +137,7 @@ void frames_release(rg_frames *f) {
     if (f->comm_stream) (void)hipStreamSynchronize(f->comm_stream);
     if (f->side) (void)hipStreamSynchronize(f->side);
     for (void *p : f->parts) (void)hipFree(p);
+    for (void *p : f->packed) (void)hipFree(p);
     for (void *p : f->gathered) (void)hipFree(p);
     for (void *p : f->image) (void)hipFree(p);
     for (hipEvent_t e : f->rendered) (void)hipEventDestroy(e);
@@ -116,6 +182,7 @@ rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t heigh
     const uint32_t tiles = (height + tile_rows - 1) / tile_rows;
     f->slot_rows = (tiles + (uint32_t)world - 1) / (uint32_t)world * tile_rows;  // equal on every rank
     f->part_bytes = (size_t)f->slot_rows * width * 4;
+    f->slot_bytes = rg_packed_slot_bytes(f->slot_rows, width);
     bool good = true;
     auto stream = [&](hipStream_t &s) { good = good && ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)); };
     auto event = [&](std::vector<hipEvent_t> &v) {
@@ -131,13 +198,15 @@ rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t heigh
     f->render.assign(depth, nullptr);
     for (int b = 0; b < depth && good; ++b) {
         stream(f->render[b]);
-        alloc(f->parts, f->part_bytes);
+        alloc(f->parts, std::max(f->part_bytes, f->slot_bytes));  // the root sends its part's first slot_bytes
         event(f->rendered);
         event(f->sent);
         event(f->done);
         if (rank == 0) {
-            alloc(f->gathered, f->part_bytes * (size_t)world);
+            alloc(f->gathered, f->slot_bytes * (size_t)world);
             alloc(f->image, (size_t)height * width * 4);
+        } else {
+            alloc(f->packed, f->slot_bytes);
         }
     }
     stream(f->comm_stream);
@@ -160,18 +229,21 @@ rg_status rg_frames_step(rg_frames *f) {
     rg_status st = rg_render_tiles_async(f->scene, f->w, f->h, &f->tiling, static_cast<uint8_t *>(f->parts[b]),
                                          nullptr, rs, nullptr);
     if (st != RG_OK) return st;
+    // off the root the part travels packed (3 B per pixel); the root's own part is read in place
+    if (f->rank != 0 && !ok(rg_launch_pack_rgb(f->parts[b], f->packed[b], (size_t)f->slot_rows * f->w, rs)))
+        return RG_ERR_DEVICE;
     if (!ok(hipEventRecord(f->rendered[b], rs)) || !ok(hipStreamWaitEvent(f->comm_stream, f->rendered[b], 0)))
         return RG_ERR_DEVICE;
     // ncclUint8 = 1 (rccl.h); recvbuff may be NULL off the root.  ncclSuccess = 0;
     // a non-blocking communicator may answer ncclInProgress = 7 with the operation enqueued
-    const int gr = f->gather(f->parts[b], f->rank == 0 ? f->gathered[b] : nullptr, f->part_bytes, 1, 0, f->comm,
-                             f->comm_stream);
+    const int gr = f->gather(f->rank == 0 ? f->parts[b] : f->packed[b], f->rank == 0 ? f->gathered[b] : nullptr,
+                             f->slot_bytes, 1, 0, f->comm, f->comm_stream);
     if (gr != 0 && gr != 7) return RG_ERR_DEVICE;
     if (!ok(hipEventRecord(f->sent[b], f->comm_stream))) return RG_ERR_DEVICE;
     if (f->rank == 0) {
         if (!ok(hipStreamWaitEvent(f->side, f->sent[b], 0))) return RG_ERR_DEVICE;
-        if (!ok(rg_launch_reinterleave(f->gathered[b], f->image[b], f->w, f->h, f->T, (uint32_t)f->world, f->slot_rows,
-                                       f->side)) ||
+        if (!ok(rg_launch_reinterleave(f->gathered[b], f->parts[b], f->image[b], f->w, f->h, f->T,
+                                       (uint32_t)f->world, f->slot_bytes, f->side)) ||
             !ok(hipEventRecord(f->done[b], f->side)))
             return RG_ERR_DEVICE;
     } else if (!ok(hipEventRecord(f->done[b], f->comm_stream))) {

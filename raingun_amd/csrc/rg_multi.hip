@@ -4,7 +4,8 @@
 // The frame is cut into tile_rows-row tiles dealt round-robin (tile t ->
 // device t % N, the balance argument of DESIGN.md §6).  Per call:
 //   device i, stream i : render its tiles into part[i] (its replica of the scene)
-//   all devices        : ONE ncclGather of the equal-size parts to device 0
+//   all devices        : ONE ncclGather of the equal-size parts to device 0, packed to
+//                        RGB (3 B per pixel: alpha is always 255) off device 0
 //                        (ncclGroupStart/End: one thread issues N ranks' calls)
 //   device 0, stream 0 : re-interleave gathered parts into the frame, then
 //                        copy the frame to the caller's host buffer
@@ -25,8 +26,12 @@
 #include "../../include/raingun.h"
 #include "rg_internal.h"
 
-hipError_t rg_launch_reinterleave(const void *gathered, void *image, uint32_t width, uint32_t height, uint32_t tile_rows,
-                                  uint32_t world, uint32_t slot_rows, hipStream_t stream);  // rg_frames.hip
+// rg_frames.hip: parts travel as packed RGB (3 B per pixel); device 0 reads its own part in place
+hipError_t rg_launch_reinterleave(const void *gathered, const void *root_part, void *image, uint32_t width,
+                                  uint32_t height, uint32_t tile_rows, uint32_t world, size_t slot_bytes,
+                                  hipStream_t stream);
+hipError_t rg_launch_pack_rgb(const void *rgba, void *rgb, size_t npx, hipStream_t stream);
+size_t rg_packed_slot_bytes(uint32_t slot_rows, uint32_t width);
 
 namespace {
 
@@ -94,12 +99,13 @@ constexpr int kNcclInProgress = 7;  // a non-blocking communicator's "enqueued"
 struct rg_multi_res {
     int n = 0;
     uint32_t w = 0, h = 0, T = 0, slot_rows = 0;
-    size_t part_bytes = 0;
+    size_t part_bytes = 0;   // RGBA part
+    size_t slot_bytes = 0;   // packed RGB part each device sends
     std::vector<int> devs;
     std::vector<rg_scene *> reps;      // reps[0] = the scene itself (not owned)
     std::vector<void *> comms;
     std::vector<hipStream_t> streams;
-    std::vector<void *> parts;
+    std::vector<void *> parts, packed;            // packed[0] unused: device 0's part is read in place
     void *gathered = nullptr, *image = nullptr;  // device 0
     unsigned long long *snap = nullptr;          // pinned: 4 words per device
     hipEvent_t ev0 = nullptr, ev1 = nullptr;     // device 0: render start .. frame assembled
@@ -118,6 +124,7 @@ void free_res(rg_multi_res *m) {
         (void)hipSetDevice(m->devs[i]);
         if (i < (int)m->comms.size() && m->comms[i] && r) (void)r->destroy(m->comms[i]);
         if (i < (int)m->parts.size() && m->parts[i]) (void)hipFree(m->parts[i]);
+        if (i < (int)m->packed.size() && m->packed[i]) (void)hipFree(m->packed[i]);
         if (i < (int)m->streams.size() && m->streams[i]) (void)hipStreamDestroy(m->streams[i]);
         if (i > 0 && i < (int)m->reps.size() && m->reps[i]) rg_scene_free(m->reps[i]);
     }
@@ -147,24 +154,28 @@ rg_status build_res(const rg_scene *s, int n, uint32_t W, uint32_t H, uint32_t T
     const uint32_t tiles = (H + T - 1) / T;
     m->slot_rows = (tiles + (uint32_t)n - 1) / (uint32_t)n * T;  // equal on every device
     m->part_bytes = (size_t)m->slot_rows * W * 4;
+    m->slot_bytes = rg_packed_slot_bytes(m->slot_rows, W);
     for (int i = 0; i < n; ++i) m->devs.push_back((s->device + i) % ndev);
     m->reps.assign(n, nullptr);
     m->comms.assign(n, nullptr);
     m->streams.assign(n, nullptr);
     m->parts.assign(n, nullptr);
+    m->packed.assign(n, nullptr);
     m->reps[0] = const_cast<rg_scene *>(s);
     rg_status st = RG_OK;
     for (int i = 1; i < n && st == RG_OK; ++i) st = rg_scene_replica(s, m->devs[i], &m->reps[i]);
     for (int i = 0; i < n && st == RG_OK; ++i) {
         if (!ok(hipSetDevice(m->devs[i])) || !ok(hipStreamCreateWithFlags(&m->streams[i], hipStreamNonBlocking)))
             st = RG_ERR_DEVICE;
-        else if (!ok(hipMalloc(&m->parts[i], m->part_bytes)) || !ok(hipMemset(m->parts[i], 0, m->part_bytes)))
+        else if (!ok(hipMalloc(&m->parts[i], std::max(m->part_bytes, m->slot_bytes))) ||
+                 !ok(hipMemset(m->parts[i], 0, std::max(m->part_bytes, m->slot_bytes))) ||
+                 (i > 0 && !ok(hipMalloc(&m->packed[i], m->slot_bytes))))
             st = RG_ERR_OUT_OF_MEMORY;  // padding rows of the last tiles stay zero
     }
     if (st == RG_OK) {
         void *snap = nullptr;
         (void)hipSetDevice(m->devs[0]);
-        if (!ok(hipMalloc(&m->gathered, m->part_bytes * (size_t)n)) || !ok(hipMalloc(&m->image, (size_t)H * W * 4)) ||
+        if (!ok(hipMalloc(&m->gathered, m->slot_bytes * (size_t)n)) || !ok(hipMalloc(&m->image, (size_t)H * W * 4)) ||
             !ok(hipHostMalloc(&snap, (size_t)n * 4 * sizeof(unsigned long long), hipHostMallocPortable)))
             st = RG_ERR_OUT_OF_MEMORY;
         m->snap = static_cast<unsigned long long *>(snap);
@@ -215,13 +226,16 @@ extern "C" rg_status rg_render_multi(const rg_scene *s, uint32_t W, uint32_t H, 
         rg_status st = rg_launch_tiles(m->reps[i], W, H, &t, static_cast<uint8_t *>(m->parts[i]), nullptr,
                                        m->streams[i], m->snap + 4 * i, nullptr);
         if (st != RG_OK) return st;
+        if (i > 0 && !ok(rg_launch_pack_rgb(m->parts[i], m->packed[i], (size_t)m->slot_rows * W, m->streams[i])))
+            return RG_ERR_DEVICE;
     }
     // one gather of the equal-size parts to device 0 (all ranks' calls in one group)
     if (r->group_start() != 0) return RG_ERR_COLLECTIVE;
     int gerr = 0;
     for (int i = 0; i < n; ++i) {
         (void)hipSetDevice(m->devs[i]);
-        const int g = r->gather(m->parts[i], i == 0 ? m->gathered : nullptr, m->part_bytes, kNcclUint8, 0, m->comms[i],
+        const int g = r->gather(i == 0 ? m->parts[i] : m->packed[i], i == 0 ? m->gathered : nullptr, m->slot_bytes,
+                                kNcclUint8, 0, m->comms[i],
                                 m->streams[i]);
         if (g != 0 && g != kNcclInProgress && gerr == 0) gerr = g;
     }
@@ -229,7 +243,8 @@ extern "C" rg_status rg_render_multi(const rg_scene *s, uint32_t W, uint32_t H, 
     if (gerr != 0 || (ge != 0 && ge != kNcclInProgress)) return RG_ERR_COLLECTIVE;
     // device 0: re-interleave, copy to the host
     if (!ok(hipSetDevice(m->devs[0])) ||
-        !ok(rg_launch_reinterleave(m->gathered, m->image, W, H, T, (uint32_t)n, m->slot_rows, m->streams[0])) ||
+        !ok(rg_launch_reinterleave(m->gathered, m->parts[0], m->image, W, H, T, (uint32_t)n, m->slot_bytes,
+                                   m->streams[0])) ||
         !ok(hipEventRecord(m->ev1, m->streams[0])) ||
         !ok(hipMemcpyAsync(rgba_out, m->image, (size_t)H * W * 4, hipMemcpyDeviceToHost, m->streams[0])))
         return RG_ERR_DEVICE;

@@ -67,8 +67,9 @@ def _hip_runtime():
 
 def _fake_gather(world, others, calls):
     """A stand-in for ncclGather on rank 0 of `world` ranks: slot 0 of the
-    receive buffer gets this rank's part, slot r the pre-rendered part of rank
-    r -- device copies on the stream the pipeline hands over, as RCCL would."""
+    receive buffer gets this rank's send buffer, slot r rank r's pre-rendered
+    part as that rank would send it (`others[r]`, packed RGB) -- device copies
+    on the stream the pipeline hands over, as RCCL would."""
     hip = _hip_runtime()
 
     def gather(send, recv, count, dtype, root, comm, stream):
@@ -100,11 +101,15 @@ def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, de
     ref = ds.render_image(w, h)
     lib = _abi.lib()
     slot = rd.slot_rows(h, world, T)
-    others = [torch.zeros((slot, w, 4), dtype=torch.uint8, device="cuda") for _ in range(world)]
+    slot_bytes = (slot * w * 3 + 15) // 16 * 16  # off the root a part travels as packed RGB (rg_frames.hip)
+    parts = [torch.zeros((slot, w, 4), dtype=torch.uint8, device="cuda") for _ in range(world)]
+    others = [torch.zeros(slot_bytes, dtype=torch.uint8, device="cuda") for _ in range(world)]
     for r in range(1, world):
         t = _abi.rg_tiling(T, world, r)
-        _abi.check(lib.rg_render_tiles_async(ds.handle, w, h, C.byref(t), C.c_void_p(others[r].data_ptr()), None,
+        _abi.check(lib.rg_render_tiles_async(ds.handle, w, h, C.byref(t), C.c_void_p(parts[r].data_ptr()), None,
                                              None, None))
+        torch.cuda.synchronize()
+        others[r][:slot * w * 3] = parts[r][..., :3].reshape(-1)
     torch.cuda.synchronize()
     calls = []
     fn = _fake_gather(world, others, calls)
@@ -120,7 +125,7 @@ def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, de
     _abi.check(lib.rg_frames_flush(hdl))
     lib.rg_frames_destroy(hdl)
     ds.close()
-    assert calls and all(c == slot * w * 4 for c in calls)
+    assert calls and all(c == slot_bytes for c in calls)
 
 
 def test_native_pipeline_reports_device_errors():
