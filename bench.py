@@ -207,6 +207,9 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     steps = args.steps if steps is None else steps
     warmup = args.warmup if warmup is None else warmup
     scene, label, src, body_counts, ops_per_ray = load_workload(workload, W, H)
+    if args.depth is not None:  # diagnostic: override the recursion cap
+        scene.max_recursion_depth = args.depth
+        label += f" (depth overridden: {args.depth})"
     ds = DeviceScene(scene, device=local_rank)  # scene + textures uploaded once, resident in HBM
     if args.tile_order >= 0:
         ds.set_tile_order(args.tile_order)
@@ -532,6 +535,7 @@ def main() -> None:
                     help="rows per interleaved row tile of the N-way split (8: the slowest of 8 shares is 2-4 %% "
                          "faster than with 16, profiles/r01/bench_rank_shares.txt)")
     ap.add_argument("--share-rank", type=int, default=0, help="diagnostic: which rank's share --share times")
+    ap.add_argument("--depth", type=int, default=None, help="diagnostic: override the workload's recursion depth")
     ap.add_argument("--tile-order", type=int, default=-1,
                     help="diagnostic: 1 = probe-ordered tiles, 0 = raster order, -1 = library default")
     ap.add_argument("--share", type=int, default=1,

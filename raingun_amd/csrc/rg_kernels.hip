@@ -160,6 +160,7 @@ struct SphScalar {
     const RG_CONST RgBox *bx;
     const RG_CONST RgBvhNode *nd;
     __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
+    __device__ __forceinline__ RgBvhNode getn_uniform(int i) const { return nd[i]; }
     __device__ __forceinline__ RgSph getv(int i) const { return ((const RgSph *)s)[i]; }
     __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
     __device__ __forceinline__ RgDsk getd(int i) const { return dk[i]; }
@@ -178,6 +179,17 @@ struct SphLds {
     const RgDsk *dk;
     const RgBox *bx;
     const RgBvhNode *nd;
+#ifndef RG_WAVE_NODE_SCALAR
+#define RG_WAVE_NODE_SCALAR 0
+#endif
+#if RG_WAVE_NODE_SCALAR
+    // the wave-coherent walk's node (wave-uniform index) through scalar loads:
+    // SGPR operands for the box tests instead of 32 broadcast VGPRs
+    const RG_CONST RgBvhNode *nds;
+    __device__ __forceinline__ RgBvhNode getn_uniform(int i) const { return nds[i]; }
+#else
+    __device__ __forceinline__ RgBvhNode getn_uniform(int i) const { return nd[i]; }
+#endif
     __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
     __device__ __forceinline__ RgSph getv(int i) const { return s[i]; }
     __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
@@ -514,7 +526,7 @@ __device__ __forceinline__ void bvh_spheres(const RgKernelArgs &a, const Src &sr
     [[maybe_unused]] const unsigned long long t_in = RG_CLOCK();
     for (;;) {
         RG_STAT(5, 1);
-        const RgBvhNode N = src.getn(node);
+        const RgBvhNode N = src.getn_uniform(node);
         const int nch = wave_uniform(N.nchild);
         const float tb = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
         int next = -1;
@@ -588,6 +600,10 @@ __device__ __forceinline__ void cswap(uint32_t &x, uint32_t &y) {
     y = hi;
 }
 
+#ifndef RG_LANE_LEAF_BATCH
+#define RG_LANE_LEAF_BATCH 0  // 1: the per-lane walk postpones leaf tests and runs them in batches (below)
+#endif
+
 template <class Src>
 __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, V3 o, V3 d, bool shadow, double ld,
                                          double t0s, Closest &c, bool &occl, bool &need) {
@@ -603,10 +619,94 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
     RG_STAT(4, 1);
     RG_STAT(7, RG_LANES(1));
     [[maybe_unused]] const unsigned long long t_in = RG_CLOCK();
+#if RG_LANE_LEAF_BATCH
+    // Speculative traversal (Aila & Laine 2009): a lane keeps the leaves a node
+    // visit finds pending and visits no further node until they are tested; the
+    // wave tests leaves only when at least as many lanes hold one as could visit
+    // a node (or none can), so a leaf round runs with many lanes instead of the
+    // few whose node happened to have leaf children.  Leaf tests commute
+    // (closest_add, any-hit), and pruning with a bound not yet tightened by the
+    // postponed leaves only culls less: results are identical.
+    int l0 = 0, l1 = 0, l2 = 0, l3 = 0, nl = 0;
+    for (;;) {
+        const bool visit = need && node >= 0 && nl == 0;
+        const bool leaf = need && nl > 0;
+        const int nv = __builtin_popcountll(__ballot(visit)), nlf = __builtin_popcountll(__ballot(leaf));
+        if (nv + nlf == 0) break;
+        RG_STAT(5, 1);
+#ifdef RG_ITER_STATS
+        {
+            if ((int)(threadIdx.x & 63u) == __builtin_ffsll((long long)__ballot(1)) - 1) {
+                atomicAdd(&a.counters[nlf >= nv ? 14 : 12], 1ull);
+                atomicAdd(&a.counters[nlf >= nv ? 15 : 13], (unsigned long long)(nlf >= nv ? nlf : nv));
+            }
+        }
+#endif
+        if (nlf >= nv) {  // leaf round: every lane holding a leaf tests one
+            if (leaf) {
+                const int v = ~l0;
+                leaf_query(a, src, v >> 3, (v & 7) + 1, o, d, rf, shadow, ld, c, occl, need);
+                l0 = l1; l1 = l2; l2 = l3;
+                --nl;
+            }
+            continue;
+        }
+        if (visit) {
+            const RgBvhNode N = src.getn(node);
+            const float tb = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
+            uint32_t e0 = ~0u, e1 = ~0u, e2 = ~0u, e3 = ~0u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float tn = 0.0f;
+                if (k < N.nchild && rg_child_hit(N, k, rb, tb, tn)) {
+                    const int ch = N.child[k];
+                    if (ch < 0) {
+                        if (nl == 0) l0 = ch;
+                        else if (nl == 1) l1 = ch;
+                        else if (nl == 2) l2 = ch;
+                        else l3 = ch;
+                        ++nl;
+                    } else {
+                        const uint32_t e = lane_key(tn, ch);
+                        if (k == 0) e0 = e;
+                        else if (k == 1) e1 = e;
+                        else if (k == 2) e2 = e;
+                        else e3 = e;
+                    }
+                }
+            }
+            cswap(e0, e1); cswap(e2, e3); cswap(e0, e2); cswap(e1, e3); cswap(e1, e2);
+            if (e3 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e3;
+            if (e2 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e2;
+            if (e1 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e1;
+            if (e0 != ~0u && (shadow || !(lane_key_t(e0) > tb))) {
+                node = (int)(e0 & mask);
+            } else {
+                node = -1;
+                while (sp > 0) {
+                    const uint32_t e = stk[(uint32_t)(--sp) * stride];
+                    if (shadow || !(lane_key_t(e) > tb)) {
+                        node = (int)(e & mask);
+                        break;
+                    }
+                }
+            }
+        }
+    }
+#else
     for (;;) {
         const bool act = need && node >= 0;
         if (!__any(act)) break;
         RG_STAT(5, 1);
+#ifdef RG_ITER_STATS  // per-lane walk: iterations, active lanes (counters[12..13])
+        {
+            const unsigned long long m = __ballot(act);
+            if ((int)(threadIdx.x & 63u) == __builtin_ffsll((long long)__ballot(1)) - 1) {
+                atomicAdd(&a.counters[12], 1ull);
+                atomicAdd(&a.counters[13], (unsigned long long)__builtin_popcountll(m));
+            }
+        }
+#endif
         if (act) {
             const RgBvhNode N = src.getn(node);
             const float tb = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
@@ -635,6 +735,15 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             // leaves first (they tighten a closest-hit bound): ONE copy of the leaf
             // test, looped max-over-lanes times, instead of one per child slot
             while (nl > 0 && need) {
+#ifdef RG_ITER_STATS  // leaf-test iterations, lanes testing a leaf (counters[14..15])
+                {
+                    const unsigned long long m = __ballot(1);
+                    if ((int)(threadIdx.x & 63u) == __builtin_ffsll((long long)m) - 1) {
+                        atomicAdd(&a.counters[14], 1ull);
+                        atomicAdd(&a.counters[15], (unsigned long long)__builtin_popcountll(m));
+                    }
+                }
+#endif
                 const int v = ~l0;
                 leaf_query(a, src, v >> 3, (v & 7) + 1, o, d, rf, shadow, ld, c, occl, need);
                 l0 = l1; l1 = l2; l2 = l3;
@@ -660,6 +769,7 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             }
         }
     }
+#endif
     RG_STAT(12, RG_CLOCK() - t_in);
 }
 
@@ -1333,6 +1443,9 @@ void rg_render_kernel(RgKernelArgs a) {
         src.dk = reinterpret_cast<const RgDsk *>(smem + a.lds_dsk);
         src.bx = reinterpret_cast<const RgBox *>(smem + a.lds_box);
         src.nd = reinterpret_cast<const RgBvhNode *>(smem + a.lds_nodes);
+#if RG_WAVE_NODE_SCALAR
+        src.nds = rg_cptr(a.nodes);
+#endif
     } else {
         src.s = rg_cptr(a.sph);
         src.cc = rg_cptr(a.sph_cc);

@@ -2,11 +2,15 @@
 // Huffman, 8-bit, 1 or 3 components).
 //
 // The reference decodes its textures with jpeg-decoder 0.1.11 through
-// image::open (raingun-lib/src/material.rs:34-47).  This decoder follows the
-// IJG/libjpeg-turbo defaults instead (what PIL uses): ISLOW integer IDCT,
-// "fancy" triangle upsampling for 2x1 / 2x2 chroma, and the fixed-point
-// YCbCr->RGB tables, so its texels equal PIL's (pinned by
-// tests/test_host_native.py on the reference's three textures).
+// image::open (raingun-lib/src/material.rs:34-47).  The default flavour
+// (RGH_JPEG_REFERENCE) restates that decoder's arithmetic -- a port of
+// stb_image: integer IDCT with 12-bit constants, triangle chroma upsampling
+// with its rounding, BT.601 YCbCr->RGB in f32 -- so the reference's golden
+// renders examples/test{1,3}.png are reproduced byte for byte
+// (tests/test_oracle_golden.py).  RGH_JPEG_LIBJPEG follows the IJG/libjpeg-turbo
+// defaults instead (what PIL uses: ISLOW IDCT, fancy upsampling, fixed-point
+// colour tables); its texels equal PIL's (tests/test_host_native.py) and it is
+// the negative control of the golden-render pin.
 #include "image_codec.h"
 
 #include <array>

@@ -27,13 +27,15 @@ def main():
         w = (C.c_uint64 * 16)()
         _abi.check(_abi.lib().rg_debug_counters(ds.handle, w))
         ds.close()
-        it, lanes, it2, lanes2, sec2, low, its, shl = (int(w[k]) for k in range(4, 12))
+        it, lanes, it2, lanes2, sec2, low, its, shl, lw_it, lw_l, lf_it, lf_l = (int(w[k]) for k in range(4, 16))
         print(json.dumps({"workload": wl, "rays": st.rays.as_dict(), "query_iterations": it,
                           "lanes_per_iteration": round(lanes / max(it, 1), 2),
                           "iterations_with_depth_ge1": it2, "lanes_per_such_iteration": round(lanes2 / max(it2, 1), 2),
                           "depth_ge1_lanes_per_such_iteration": round(sec2 / max(it2, 1), 2),
                           "share_iterations_le16_lanes": round(low / max(it, 1), 3),
-                          "iterations_with_shadow_lanes": its, "shadow_lanes_per_such": round(shl / max(its, 1), 2)}),
+                          "iterations_with_shadow_lanes": its, "shadow_lanes_per_such": round(shl / max(its, 1), 2),
+                          "lane_walk_iterations": lw_it, "lane_walk_active_lanes": round(lw_l / max(lw_it, 1), 2),
+                          "leaf_iterations": lf_it, "leaf_lanes": round(lf_l / max(lf_it, 1), 2)}),
               flush=True)
 
 
