@@ -103,6 +103,7 @@ void destroy_ctx(rg_launch_ctx *c) {
     if (c->tile_cost) (void)hipFree(c->tile_cost);
     if (c->tile_perm) (void)hipFree(c->tile_perm);
     if (c->deep) (void)hipFree(c->deep);
+    if (c->prim) (void)hipFree(c->prim);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
@@ -300,6 +301,35 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
         a.deep_stack = cx->deep;
         a.deep_stride = (uint32_t)threads;
     }
+    // primary-ray sensor coordinates per column / row (ray.rs:46-51), the
+    // kernel's expressions evaluated here once per frame size (same IEEE
+    // operations in the same order, no contraction: identical doubles)
+    if (cx->prim_w != width || cx->prim_h != height || cx->prim_fov != a.fov_adjustment || !cx->prim) {
+        const size_t n = (size_t)width + height;
+        if (n > cx->prim_cap) {
+            if (cx->prim) (void)hipFree(cx->prim);
+            cx->prim = nullptr;
+            cx->prim_cap = 0;
+            void *q = nullptr;
+            if (!ok(hipMalloc(&q, n * sizeof(double)))) { (void)hipGetLastError(); return RG_ERR_OUT_OF_MEMORY; }
+            cx->prim = static_cast<double *>(q);
+            cx->prim_cap = n;
+        }
+        std::vector<double> tab(n);
+        for (uint32_t x = 0; x < width; ++x)
+            tab[x] = ((((double)x + 0.5) / (double)width) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
+        for (uint32_t y = 0; y < height; ++y)
+            tab[(size_t)width + y] = (1.0 - (((double)y + 0.5) / (double)height) * 2.0) * a.fov_adjustment;
+        // stream-ordered: earlier launches on this stream are done with the old table
+        if (!ok(hipMemcpyAsync(cx->prim, tab.data(), n * sizeof(double), hipMemcpyHostToDevice, st)) ||
+            !ok(hipStreamSynchronize(st)))
+            return RG_ERR_DEVICE;
+        cx->prim_w = width;
+        cx->prim_h = height;
+        cx->prim_fov = a.fov_adjustment;
+    }
+    a.prim_sx = cx->prim;
+    a.prim_sy = cx->prim + width;
     if (!ok(hipMemsetAsync(cx->counters, 0, RG_COUNTER_WORDS * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
     if (timed && !ok(hipEventRecord(cx->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
     if (s->tile_order == 1 || (s->tile_order < 0 && rg_heavy_path(a))) {

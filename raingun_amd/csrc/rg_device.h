@@ -161,6 +161,10 @@ struct RgKernelArgs {
     // 55-56; profiles/r02/host_visible/d2h_probe.jsonl)
     uint32_t tile_wlog;
     uint32_t defer_px;  // 1: hold pixels in LDS, one store per finished tile (the frame is in host memory)
+    // nullable: the primary rays' sensor coordinates (ray.rs:46-51) per image
+    // column (prim_sx[x]) and row (prim_sy[y]), computed on the host with the
+    // kernel's exact expressions -- two f64 divisions per pixel become two loads
+    const double *prim_sx, *prim_sy;
 };
 
 __host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }

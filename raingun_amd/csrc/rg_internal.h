@@ -25,6 +25,10 @@ struct rg_launch_ctx {
     size_t tile_cap = 0;
     void *deep = nullptr;  // frames for depths above the compiled arrays (rg_kernels.hip FrameStack<0>)
     size_t deep_bytes = 0;
+    double *prim = nullptr;  // sensor x per column then sensor y per row (RgKernelArgs::prim_sx / prim_sy)
+    size_t prim_cap = 0;     // doubles
+    uint32_t prim_w = 0, prim_h = 0;
+    double prim_fov = 0.0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
