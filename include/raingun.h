@@ -196,7 +196,10 @@ rg_status rg_host_unregister(void *ptr);
  * Launches of one scene on DISTINCT streams may be in flight together (frames
  * in flight): each stream has its own launch state (ray counters, tile queue,
  * error word), created on the stream's first use.  Calls on one scene must
- * come from one host thread at a time. */
+ * come from one host thread at a time.  Without `stats` a launch is taken to
+ * be one of several frames in flight: trace-heavy scenes then size their
+ * persistent grid for throughput (small launches use a third of the GPU or
+ * more, with at least 32 tiles per wave) rather than for one launch's latency. */
 rg_status rg_render_tiles_async(const rg_scene *scene, uint32_t width, uint32_t height,
                                 const rg_tiling *tiling, uint8_t *rgba_dev, float *rgb_dev,
                                 void *stream, rg_stats *stats);

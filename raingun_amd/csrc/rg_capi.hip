@@ -251,7 +251,7 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
 rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
                           uint8_t *rgba_dev, float *rgb_dev, hipStream_t st, unsigned long long *snap,
                           rg_launch_ctx **ctx_out, bool timed, uint32_t *tile_flags, uint32_t frame_seq,
-                          const uint32_t *cancel, uint32_t tile_wlog, bool host_frame) {
+                          const uint32_t *cancel, uint32_t tile_wlog, bool host_frame, bool pipelined) {
     if (tile_wlog < 3 || tile_wlog > 6) return RG_ERR_INVALID_ARGUMENT;
     if (!s || !rgba_dev || width == 0 || height == 0 || !tiling_valid(tiling)) return RG_ERR_INVALID_ARGUMENT;
     if (width < height) return RG_ERR_PORTRAIT;  // ray.rs:42
@@ -280,6 +280,7 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     a.cancel = cancel;
     a.tile_wlog = tile_wlog;
     a.defer_px = host_frame ? 1u : 0u;
+    a.pipelined = pipelined ? 1u : 0u;
     const int frames = frames_needed(s->max_depth);
     // host-frame launches run the MAXD == 0 kernels (the only ones with the
     // host-frame features: rg_kernels.hip HOSTF), whose frames live in a
@@ -729,7 +730,11 @@ rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t heig
                                 uint8_t *rgba_dev, float *rgb_dev, void *stream, rg_stats *stats) {
     hipStream_t st = static_cast<hipStream_t>(stream);
     rg_launch_ctx *cx = nullptr;
-    rg_status r = rg_launch_tiles(s, width, height, tiling, rgba_dev, rgb_dev, st, nullptr, &cx, stats != nullptr);
+    // an asynchronous launch without stats is taken as one of several frames in
+    // flight (the frames pipelines, bench.py): the heavy path sizes its grid for
+    // throughput (rg_kernels.hip launch_one); a synchronous one for latency
+    rg_status r = rg_launch_tiles(s, width, height, tiling, rgba_dev, rgb_dev, st, nullptr, &cx, stats != nullptr,
+                                  nullptr, 0, nullptr, 3, false, stats == nullptr);
     if (r != RG_OK || !stats) return r;
     unsigned long long c[4];
     if (!ok(hipMemcpyAsync(c, cx->counters, sizeof c, hipMemcpyDeviceToHost, st))) return RG_ERR_DEVICE;

@@ -165,6 +165,9 @@ struct RgKernelArgs {
     // column (prim_sx[x]) and row (prim_sy[y]), computed on the host with the
     // kernel's exact expressions -- two f64 divisions per pixel become two loads
     const double *prim_sx, *prim_sy;
+    // 1: this launch is one of several frames in flight (rg_render_tiles_async):
+    // the heavy path sizes its persistent grid for throughput, not latency (launch_one)
+    uint32_t pipelined;
 };
 
 __host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }

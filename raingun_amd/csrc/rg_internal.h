@@ -159,7 +159,8 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
                           uint8_t *rgba_dev, float *rgb_dev, hipStream_t stream, unsigned long long *snap,
                           rg_launch_ctx **ctx_out, bool timed = false, uint32_t *tile_flags = nullptr,
                           uint32_t frame_seq = 0, const uint32_t *cancel = nullptr, uint32_t tile_wlog = 3,
-                          bool host_frame = false);  // host_frame: rgba_dev is page-locked host memory
+                          bool host_frame = false,   // host_frame: rgba_dev is page-locked host memory
+                          bool pipelined = false);   // frames in flight: size the grid for throughput
 
 // Ray counts and status of a counter snapshot (stats nullable).
 rg_status rg_snap_status(const unsigned long long *snap, rg_stats *stats);

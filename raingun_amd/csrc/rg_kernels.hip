@@ -1260,6 +1260,9 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 // flight too -- instead of 3072 persistent waves pinning their slots until the
 // frame's queue is empty.  0 = persistent.  16 measured best for the whole 4K
 // frame and for 1/2 .. 1/8 shares (profiles/r01/variants_light_tiles_per_wave.txt).
+#ifndef RG_PIPE_TILES_PER_WAVE
+#define RG_PIPE_TILES_PER_WAVE 32  // heavy launches with frames in flight (launch_one, RgKernelArgs::pipelined)
+#endif
 #ifndef RG_LIGHT_TILES_PER_WAVE
 #define RG_LIGHT_TILES_PER_WAVE 16
 #endif
@@ -2420,6 +2423,18 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     unsigned long long blocks = (unsigned long long)cus * per_cu;
     const unsigned long long need = (tiles + waves - 1) / waves;
     if (blocks > need) blocks = need;
+    if (LB == 1 && MAXD != 0 && a->pipelined) {
+        // Heavy path, frames in flight: each persistent block takes >= RG_PIPE_TILES_PER_WAVE
+        // tiles per wave, so its lifetime dwarfs its start (LDS staging) and its slowest
+        // wave's tail, while every launch keeps >= 1/3 of the CUs; the other frames in
+        // flight fill the rest.  North-star 1/8 share 0.440 -> 0.399 ms, 1/4 0.753 ->
+        // 0.713, 8K 1/8 1.250 -> 1.220; whole frames unchanged (profiles/r02/ab_pipe_blocks.txt)
+        const unsigned long long per = waves * RG_PIPE_TILES_PER_WAVE;
+        unsigned long long cap = (tiles + per - 1) / per;
+        const unsigned long long floor_blocks = ((unsigned long long)cus * per_cu + 2) / 3;
+        if (cap < floor_blocks) cap = floor_blocks;
+        if (blocks > cap) blocks = cap;
+    }
     constexpr unsigned long long kmax = MAXD == 0 ? 0 : LB > 1 ? RG_LIGHT_TILES_PER_WAVE : RG_HEAVY_TILES_PER_WAVE;
     if constexpr (kmax > 0)  // non-persistent: one wave per kmax tiles
         blocks = (tiles + waves * kmax - 1) / (waves * kmax);
