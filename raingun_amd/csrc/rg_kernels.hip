@@ -2483,7 +2483,10 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
     const bool heavy = rg_heavy_path(*a);
     if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream, gt);
     const unsigned long long tiles = rg_tile_count(*a);
-    const bool tasks = RG_HEAVY_TASKS && tiles < RG_HEAVY_TASK_TILES;
+    // frames in flight (pipelined): the throughput-sized grid already keeps blocks long;
+    // task splitting then costs more than it saves (1/8 share 0.400 -> 0.384 ms without:
+    // profiles/r02/ab_task_split.txt); a single small launch keeps it (its latency)
+    const bool tasks = RG_HEAVY_TASKS && tiles < RG_HEAVY_TASK_TILES && !a->pipelined;
     if (a->n_nodes > 0)
         return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, true>(a, stream, gt)
                      : launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, false>(a, stream, gt);
