@@ -316,3 +316,30 @@ def test_frames_in_flight_on_concurrent_streams(oracle_lib, example_scenes, scen
     ds.render_tiles(w, h, stats=st)
     ds.close()
     assert st.rays.as_dict() == oracle_lib.render(SceneDesc(scene), w, h)[3]
+
+
+@pytest.mark.parametrize("path, bvh, lane", PATH_BVH)
+def test_point_lights_in_plane_surfaces(oracle_lib, path, bvh, lane):
+    """Spherical lights lying exactly in plane surfaces: every shadow ray
+    towards them meets the plane at (almost) the light's own distance, so the
+    occlusion test fl(num/den) <= light distance (bodies.rs:137-148,
+    rendering.rs:152-155) is decided by the last rounding: the kernels'
+    unfused f64 division and comparison must agree with the restatement pixel
+    for pixel.  (A division-free pre-decision of this comparison was tried
+    against this test and rejected as slower: profiles/r02/heavy_path_experiments.txt.)"""
+    from raingun_amd.scene import DirectionalLight, Plane, Sphere, SphericalLight
+    rng = np.random.default_rng(23)
+    m = Material(Color.from_str("#c0c0c0"), 0.6)
+    mr = Material(Color.from_str("#ffffff"), 0.5)
+    mr.surface = "Reflecting"
+    mr.reflectivity = 0.4
+    bodies = [Plane((0.0, -2.0, 0.0), (0.0, -1.0, 0.0), m),        # floor (normal away from the camera)
+              Plane((0.0, 0.0, -30.0), (0.0, 0.0, -1.0), m)]        # back wall
+    for _ in range(40):
+        c = (rng.uniform(-9, 9), rng.uniform(-1.5, 4), rng.uniform(-25, -6))
+        bodies.append(Sphere(c, float(rng.uniform(0.3, 1.2)), mr if rng.integers(3) == 0 else m))
+    lights = [SphericalLight((1.37, -2.0, -11.3), Color.from_str("#ffeedd"), 900.0),   # in the floor
+              SphericalLight((-4.1, 2.9, -30.0), Color.from_str("#ddeeff"), 1500.0),   # in the back wall
+              DirectionalLight((0.3, -1.0, -0.5), Color.from_str("#ffffff"), 0.6)]
+    s = Scene(bodies=bodies, lights=lights, max_recursion_depth=4)
+    _compare(oracle_lib, s, 320, 180, path=path, bvh=bvh, lane=lane)
