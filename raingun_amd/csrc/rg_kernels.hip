@@ -2075,6 +2075,11 @@ void rg_render_kernel(RgKernelArgs a) {
                     atomicAdd(&a.counters[10], 1ull);
                     atomicAdd(&a.counters[11], (unsigned long long)__builtin_popcountll(shl));
                 }
+                // light path (no BVH walk words): iterations with closest-hit lanes, those lanes
+                if (LB > 1 && (all & ~shl)) {
+                    atomicAdd(&a.counters[14], 1ull);
+                    atomicAdd(&a.counters[15], (unsigned long long)__builtin_popcountll(all & ~shl));
+                }
             }
         }
 #endif

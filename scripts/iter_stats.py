@@ -35,7 +35,9 @@ def main():
                           "share_iterations_le16_lanes": round(low / max(it, 1), 3),
                           "iterations_with_shadow_lanes": its, "shadow_lanes_per_such": round(shl / max(its, 1), 2),
                           "lane_walk_iterations": lw_it, "lane_walk_active_lanes": round(lw_l / max(lw_it, 1), 2),
-                          "leaf_iterations": lf_it, "leaf_lanes": round(lf_l / max(lf_it, 1), 2)}),
+                          "leaf_iterations": lf_it, "leaf_lanes": round(lf_l / max(lf_it, 1), 2),
+                          # light path: words 14/15 count iterations with closest-hit lanes instead
+                          "light_mixed_iterations": its + lf_it - it if wl.startswith("test") else None}),
               flush=True)
 
 
