@@ -158,7 +158,7 @@ def pmc_work(key: str):
         return None
 
 
-def roofline(key: str, frame_s: float, n_gpus: int, alg_bytes: int, tex: int):
+def roofline(key: str, frame_s: float, n_gpus: int, alg_bytes: int, tex: int, alg_ops: float = 0.0):
     """Executed-work VALU roofline of the timed configuration: the issue cycles
     of every VALU instruction the frame's kernels executed (PMC, counted at
     N=1 for the whole frame, which the N ranks split) over the cycles N GPUs
@@ -167,9 +167,19 @@ def roofline(key: str, frame_s: float, n_gpus: int, alg_bytes: int, tex: int):
     res = {"bound": "valu", "achieved": None, "peak": round(FP64_PEAK_TOPS * n_gpus, 3),
            "unit": "T FP64-rate VALU lane-ops/s", "frac": None, "traffic": None,
            "basis": "not profiled (run scripts/pmc_work.sh for this workload)"}
+    if alg_ops:
+        # SURVEY.md 8(d)'s algorithmic figure: the reference's brute-force FP64 ops per ray
+        # (16 per sphere, 14 per plane ...) x rays per frame over the FP64 lane-op peak.  Shading
+        # is not counted and the BVH skips most of the brute-force work, so it is not a
+        # utilisation figure (it exceeds 1 on the sphere scenes)
+        res["algorithmic_frac"] = round(alg_ops / frame_s / (FP64_PEAK_TOPS * 1e12 * n_gpus), 5)
     if w:
         cyc = w["valu_cycles_per_frame"]
         frac = cyc / (frame_s * n_gpus * SIMDS * CLOCK_HZ)
+        c = w.get("counters_per_frame", {})
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:  # KiB per frame as collected
+            res["traffic_raw"] = {"fetch_size_bytes": round(c["FETCH_SIZE"] * 1024), "write_size_bytes":
+                                  round(c["WRITE_SIZE"] * 1024), "fetch_correction": "x2 in traffic (gfx950)"}
         res.update({
             "achieved": round(cyc * 16.0 / frame_s / 1e12, 4),
             "frac": round(frac, 5),
@@ -237,13 +247,21 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     stream = torch.cuda.current_stream(dev)
     sh = C.c_void_p(stream.cuda_stream)
 
-    def render(stats=None, buf=None):
+    pipelined_fn = getattr(lib, "rg_render_tiles_pipelined", None)
+
+    def render(stats=None, buf=None, pipelined=False):
         # on the current stream: the frame pipeline's render stream for this frame, or the default
         dst = out if buf is None else buf
         cur = torch.cuda.current_stream(dev)
         sh_cur = sh if cur == stream else C.c_void_p(cur.cuda_stream)
-        st = lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(dst.data_ptr()), None, sh_cur,
-                                       C.byref(stats) if stats is not None else None)
+        if pipelined and pipelined_fn is not None:  # one of F frames in flight: grid sized for throughput
+            st = pipelined_fn(ds.handle, W, H, C.byref(tiling), C.c_void_p(dst.data_ptr()), None, sh_cur)
+        elif pipelined:  # a pre-round-3 library (A/B runs): a launch without stats was the pipelined one
+            st = lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(dst.data_ptr()), None,
+                                           sh_cur, None)
+        else:  # one launch sized for its own latency
+            st = lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(dst.data_ptr()), None,
+                                           sh_cur, C.byref(stats) if stats is not None else None)
         _abi.check(st, "rg_render_tiles_async")
 
     def render_tiles(_t):
@@ -262,7 +280,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     native = use_pipe and gather and args.backend == "nccl" and not args.python_pipeline
     if native:  # the per-frame loop in C++ (include/raingun_frames.h): render, ncclGather, re-interleave
         try:
-            pipe = rd.NativeFramePipeline(ds.handle, W, H, rank, world, TR, depth=F, device=dev)
+            pipe = rd.NativeFramePipeline(ds, W, H, rank, world, TR, depth=F, device=dev)
         except Exception as e:  # e.g. no communicator pointer from this torch build: same loop in Python
             print(f"[bench] native frame pipeline unavailable ({e}); using the Python loop", file=sys.stderr)
             native = False
@@ -274,7 +292,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         if native:
             pipe.step()
         elif pipe is not None:
-            pipe.step(lambda part: render(buf=part))
+            pipe.step(lambda part: render(buf=part, pipelined=True))
         else:
             rd.render_frame(render_tiles, H, rank, world, TR, out=frame, gather_bufs=gathered)
 
@@ -336,9 +354,10 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
             st_, px_ = ds.stream_status(s_.cuda_stream)
             _abi.check(st_, f"frame render (first erroring pixel {px_})")
 
-    # Single-stream kernel time (one launch after another, HIP events on that
-    # stream): the time ONE launch of this rank's share takes on an otherwise
-    # idle GPU (rocprofv3 of `--frames-in-flight 1` gives the same average).
+    # Single-stream kernel time (one latency-sized launch after another, HIP
+    # events on that stream): the time ONE launch of this rank's share takes on
+    # an otherwise idle GPU (rocprofv3 of `--frames-in-flight 1` gives the same
+    # average).  Not the timed configuration (F frames in flight).
     events = []
     for _ in range(max(1, args.roofline_frames)):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -401,7 +420,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     alg_bytes = H * W * 4  # the frame written once (all ranks together)
     key = f"{workload}@{W}x{H}"
     roof, roof_hbm = roofline(key, frame_s, world if split == world else 1, alg_bytes if split == world else
-                              my_rows * W * 4, tex)
+                              my_rows * W * 4, tex, alg_ops=rays_per_frame * ops_per_ray if split == world else 0.0)
     if split != world:  # --share diagnostic: the PMC figures are whole-frame ones
         roof.update({"achieved": None, "frac": None, "traffic": None, "basis": "--share diagnostic: not computed"})
     ref_equiv = my_rays * ops_per_ray / (kernel_ms * 1e-3) / 1e12
@@ -411,6 +430,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         "steps": steps,
         "warmup": warmup,
         "kernel_ms": round(kernel_ms, 4),
+        "kernel_ms_config": "one latency-sized launch at a time on one stream (rg_render_tiles_async), HIP events",
         "data": src,
         "settle_s": args.settle_s,
         "config": {"workload": label, "width": W, "height": H, "max_recursion_depth": scene.max_recursion_depth,

@@ -196,13 +196,20 @@ rg_status rg_host_unregister(void *ptr);
  * Launches of one scene on DISTINCT streams may be in flight together (frames
  * in flight): each stream has its own launch state (ray counters, tile queue,
  * error word), created on the stream's first use.  Calls on one scene must
- * come from one host thread at a time.  Without `stats` a launch is taken to
- * be one of several frames in flight: trace-heavy scenes then size their
- * persistent grid for throughput (small launches use a third of the GPU or
- * more, with at least 32 tiles per wave) rather than for one launch's latency. */
+ * come from one host thread at a time.  The launch is sized for its own
+ * latency (the whole GPU for this one frame). */
 rg_status rg_render_tiles_async(const rg_scene *scene, uint32_t width, uint32_t height,
                                 const rg_tiling *tiling, uint8_t *rgba_dev, float *rgb_dev,
                                 void *stream, rg_stats *stats);
+
+/* rg_render_tiles_async for a caller that keeps several frames in flight on
+ * distinct streams (rg_frames, bench.py): asynchronous, and trace-heavy scenes
+ * size their persistent grid for throughput -- a small launch takes a third
+ * of the GPU or more with at least 32 tiles per wave, and the other frames in
+ * flight fill the rest -- rather than for one launch's latency.  Same output. */
+rg_status rg_render_tiles_pipelined(const rg_scene *scene, uint32_t width, uint32_t height,
+                                    const rg_tiling *tiling, uint8_t *rgba_dev, float *rgb_dev,
+                                    void *stream);
 
 /* Forget the launch state of `stream` (before the caller destroys that stream);
  * the null stream's state lives as long as the scene. */

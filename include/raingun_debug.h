@@ -61,6 +61,16 @@ rg_status rg_debug_set_image_bands(rg_scene *scene, int32_t bands);
  * row segments per PCIe write.  Device-resident renders always use 8x8. */
 rg_status rg_debug_set_host_tile_shape(rg_scene *scene, int32_t tile_wlog);
 
+/* rg_render_multi: mode 0 (default) = every device copies its rows of the
+ * frame to the host buffer itself, over its own PCIe link, in `bands` row
+ * bands per device (0 = automatic, 1..4) overlapped with the later bands'
+ * renders; mode 1 = ONE RCCL ncclGather of the parts to the scene's device,
+ * re-interleave there, one copy to the host.  stand_in = 1 places every
+ * "device" on the scene's device (a replica each) and routes mode 1's gather
+ * through a stand-in with ncclGather's signature and group semantics, so
+ * ngpus > 1 runs on one GPU (tests).  Results are identical for every setting. */
+rg_status rg_debug_set_multi(rg_scene *scene, int32_t mode, int32_t stand_in, int32_t bands);
+
 /* Copy the scene's 16 statistics words after the last render: [0..2] ray
  * counts, [4..8] BVH traversal statistics when the library was built with
  * -DRG_BVH_STATS (zero otherwise). */

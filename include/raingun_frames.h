@@ -33,7 +33,11 @@ typedef struct rg_frames rg_frames;
 
 /* Set up `depth` frames in flight of a width x height frame split into
  * tile_rows-row tiles over `world` ranks (this is rank `rank`).  `comm` is an
- * ncclComm_t over the same ranks, `gather` the matching ncclGather. */
+ * ncclComm_t over the same ranks, `gather` the matching ncclGather.
+ * Lifetime: destroy the frames before their scene.  If the scene is destroyed
+ * first, it waits for the frames' renders and detaches them: every later call
+ * but rg_frames_destroy (which then frees only the frames' own resources)
+ * returns RG_ERR_INVALID_ARGUMENT. */
 rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t height, uint32_t tile_rows, int32_t rank,
                            int32_t world, int32_t depth, void *comm, rg_gather_fn gather, rg_frames **out);
 void rg_frames_destroy(rg_frames *frames);

@@ -125,6 +125,7 @@ EXPORTED_SYMBOLS = (
     "rg_scene_set_max_depth",
     "rg_render_image",
     "rg_render_tiles_async",
+    "rg_render_tiles_pipelined",
     "rg_render_tiles",
     "rg_tiling_rows",
     "rg_render_stream",
@@ -138,7 +139,7 @@ EXPORTED_SYMBOLS = (
 # include/raingun_debug.h
 DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
                  "rg_debug_set_tile_order", "rg_debug_set_lane_depth", "rg_debug_set_image_bands",
-                 "rg_debug_set_host_tile_shape")
+                 "rg_debug_set_host_tile_shape", "rg_debug_set_multi")
 # include/raingun_frames.h
 FRAMES_SYMBOLS = ("rg_frames_create", "rg_frames_destroy", "rg_frames_step", "rg_frames_flush", "rg_frames_image",
                   "rg_frames_read_image", "rg_frames_status")
@@ -174,6 +175,10 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_render_tiles_async.restype = C.c_int32
     lib.rg_render_tiles_async.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(rg_tiling), C.c_void_p,
                                           C.c_void_p, C.c_void_p, P(rg_stats)]
+    if hasattr(lib, "rg_render_tiles_pipelined"):  # absent from pre-round-3 builds (A/B runs against them)
+        lib.rg_render_tiles_pipelined.restype = C.c_int32
+        lib.rg_render_tiles_pipelined.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(rg_tiling), C.c_void_p,
+                                                  C.c_void_p, C.c_void_p]
     lib.rg_render_tiles.restype = C.c_int32
     lib.rg_render_tiles.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(rg_tiling), C.c_void_p, C.c_void_p,
                                     P(rg_stats)]
@@ -194,6 +199,9 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_set_lane_depth.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_set_image_bands.restype = C.c_int32
     lib.rg_debug_set_image_bands.argtypes = [C.c_void_p, C.c_int32]
+    if hasattr(lib, "rg_debug_set_multi"):  # absent from pre-round-3 builds
+        lib.rg_debug_set_multi.restype = C.c_int32
+        lib.rg_debug_set_multi.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
     if hasattr(lib, "rg_debug_set_host_tile_shape"):  # absent from older builds A/B runs load (RAINGUN_HIP_LIB)
         lib.rg_debug_set_host_tile_shape.restype = C.c_int32
         lib.rg_debug_set_host_tile_shape.argtypes = [C.c_void_p, C.c_int32]

@@ -130,6 +130,8 @@ void release_image_res(rg_image_res &r) {
 void release(rg_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
+    for (rg_frames *f : s->frames) rg_frames_detach_scene(f);
+    s->frames.clear();
     rg_multi_release(s);
     release_image_res(s->img);
     for (void *p : s->allocations) (void)hipFree(p);
@@ -147,9 +149,16 @@ rg_launch_ctx *ctx_for(const rg_scene *s, hipStream_t stream) {
     if (!c) return nullptr;
     c->stream = stream;
     void *p = nullptr, *q = nullptr;
-    if (!ok(hipMalloc(&p, RG_COUNTER_WORDS * sizeof(unsigned long long)))) { delete c; return nullptr; }
+    if (!ok(hipMalloc(&p, 2 * RG_COUNTER_WORDS * sizeof(unsigned long long)))) { delete c; return nullptr; }
     c->counters = static_cast<unsigned long long *>(p);
-    if (!ok(hipMalloc(&q, sizeof(unsigned long long))) || !ok(hipMemset(q, 0, sizeof(unsigned long long)))) {
+    c->last_counters = c->counters;
+    // stream-ordered: hipMemset on the null stream does not order against a
+    // non-blocking stream's first launch
+    if (!ok(hipMemsetAsync(p, 0, 2 * RG_COUNTER_WORDS * sizeof(unsigned long long), stream))) {
+        destroy_ctx(c);
+        return nullptr;
+    }
+    if (!ok(hipMalloc(&q, sizeof(unsigned long long))) || !ok(hipMemsetAsync(q, 0, sizeof(unsigned long long), stream))) {
         if (q) (void)hipFree(q);
         destroy_ctx(c);
         return nullptr;
@@ -251,11 +260,15 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
 rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
                           uint8_t *rgba_dev, float *rgb_dev, hipStream_t st, unsigned long long *snap,
                           rg_launch_ctx **ctx_out, bool timed, uint32_t *tile_flags, uint32_t frame_seq,
-                          const uint32_t *cancel, uint32_t tile_wlog, bool host_frame, bool pipelined) {
+                          const uint32_t *cancel, uint32_t tile_wlog, bool host_frame, bool pipelined,
+                          uint32_t tile_first, uint32_t tile_count) {
     if (tile_wlog < 3 || tile_wlog > 6) return RG_ERR_INVALID_ARGUMENT;
     if (!s || !rgba_dev || width == 0 || height == 0 || !tiling_valid(tiling)) return RG_ERR_INVALID_ARGUMENT;
     if (width < height) return RG_ERR_PORTRAIT;  // ray.rs:42
-    const uint32_t out_rows = rg_tiling_rows(height, tiling);
+    const uint32_t sel_rows = rg_tiling_rows(height, tiling);  // every selected tile
+    const uint32_t sel_tiles = sel_rows / tiling->tile_rows;
+    if (tile_first > sel_tiles) return RG_ERR_INVALID_ARGUMENT;
+    const uint32_t out_rows = std::min(sel_tiles - tile_first, tile_count) * tiling->tile_rows;
     if ((unsigned long long)out_rows * width >= (1ull << 32) || (unsigned long long)height * width >= (1ull << 32))
         return RG_ERR_INVALID_ARGUMENT;  // the reference's u32 pixel index (rendering.rs:27)
     if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
@@ -264,15 +277,19 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     s->last = cx;
     if (ctx_out) *ctx_out = cx;
     RgKernelArgs a = rg_make_args(s);
-    a.counters = cx->counters;
+    a.counters = cx->counters + (size_t)cx->cur * RG_COUNTER_WORDS;  // zero (see rg_launch_ctx::counters)
+    a.counters_next = cx->counters + (size_t)(1 - cx->cur) * RG_COUNTER_WORDS;
     a.err_sticky = cx->sticky;
     a.width = width;
     a.height = height;
     a.tile_rows = tiling->tile_rows;
     a.tile_stride = tiling->tile_stride;
     a.tile_offset = tiling->tile_offset;
+    a.tile_base = tile_first;
     a.out_rows = out_rows;
     a.aspect = (double)width / (double)height;
+    a.width_d = (double)width;
+    a.height_d = (double)height;
     a.rgba = reinterpret_cast<uint32_t *>(rgba_dev);
     a.rgb = rgb_dev;
     a.tile_flags = tile_flags;
@@ -331,11 +348,13 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     }
     a.prim_sx = cx->prim;
     a.prim_sy = cx->prim + width;
-    if (!ok(hipMemsetAsync(cx->counters, 0, RG_COUNTER_WORDS * sizeof(unsigned long long), st))) return RG_ERR_DEVICE;
     if (timed && !ok(hipEventRecord(cx->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
     if (s->tile_order == 1 || (s->tile_order < 0 && rg_heavy_path(a))) {
         const size_t ntiles = (size_t)rg_tile_count(a);
-        if (ntiles > cx->tile_cap) {
+        const rg_launch_ctx::PermKey key{width, height, tiling->tile_rows, tiling->tile_stride, tiling->tile_offset,
+                                         tile_first, out_rows, tile_wlog, s->max_depth, (uint32_t)s->n_lights,
+                                         a.fov_adjustment, s->mats};
+        if (!(cx->perm_valid && cx->perm_key == key) && ntiles > cx->tile_cap) {
             if (cx->tile_cost) (void)hipFree(cx->tile_cost);
             if (cx->tile_perm) (void)hipFree(cx->tile_perm);
             cx->tile_cost = cx->tile_perm = nullptr;
@@ -346,13 +365,24 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
             cx->tile_cap = ntiles;
         }
         if (ntiles > 0) {
-            if (!ok(rg_launch_tile_order(&a, cx->tile_cost, cx->tile_perm, st))) return RG_ERR_DEVICE;
+            // the order depends only on the frame geometry and the scene: made once per
+            // launch context and key, so a steady stream of frames runs ONE kernel each
+            if (!(cx->perm_valid && cx->perm_key == key)) {
+                cx->perm_valid = false;
+                if (!ok(rg_launch_tile_order(&a, cx->tile_cost, cx->tile_perm, st))) return RG_ERR_DEVICE;
+                cx->perm_valid = true;
+                cx->perm_key = key;
+            }
             a.tile_perm = cx->tile_perm;
         }
     }
-    if (out_rows > 0 && !ok(rg_launch_render(&a, disp, st))) return RG_ERR_DEVICE;
+    cx->last_counters = a.counters;
+    if (out_rows > 0) {
+        if (!ok(rg_launch_render(&a, disp, st))) return RG_ERR_DEVICE;
+        cx->cur = 1 - cx->cur;  // the kernel zeroes the other set for the next launch
+    }
     if (timed && !ok(hipEventRecord(cx->ev1, st))) return RG_ERR_DEVICE;
-    if (snap && !ok(hipMemcpyAsync(snap, cx->counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st)))
+    if (snap && !ok(hipMemcpyAsync(snap, a.counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st)))
         return RG_ERR_DEVICE;
     return RG_OK;
 }
@@ -730,19 +760,24 @@ rg_status rg_render_tiles_async(const rg_scene *s, uint32_t width, uint32_t heig
                                 uint8_t *rgba_dev, float *rgb_dev, void *stream, rg_stats *stats) {
     hipStream_t st = static_cast<hipStream_t>(stream);
     rg_launch_ctx *cx = nullptr;
-    // an asynchronous launch without stats is taken as one of several frames in
-    // flight (the frames pipelines, bench.py): the heavy path sizes its grid for
-    // throughput (rg_kernels.hip launch_one); a synchronous one for latency
     rg_status r = rg_launch_tiles(s, width, height, tiling, rgba_dev, rgb_dev, st, nullptr, &cx, stats != nullptr,
-                                  nullptr, 0, nullptr, 3, false, stats == nullptr);
+                                  nullptr, 0, nullptr, 3, false, false);
     if (r != RG_OK || !stats) return r;
     unsigned long long c[4];
-    if (!ok(hipMemcpyAsync(c, cx->counters, sizeof c, hipMemcpyDeviceToHost, st))) return RG_ERR_DEVICE;
+    if (!ok(hipMemcpyAsync(c, cx->last_counters, sizeof c, hipMemcpyDeviceToHost, st))) return RG_ERR_DEVICE;
     if (!ok(hipStreamSynchronize(st))) return RG_ERR_DEVICE;
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, cx->ev0, cx->ev1);
     stats->kernel_ms = ms;
     return rg_snap_status(c, stats);
+}
+
+rg_status rg_render_tiles_pipelined(const rg_scene *s, uint32_t width, uint32_t height, const rg_tiling *tiling,
+                                    uint8_t *rgba_dev, float *rgb_dev, void *stream) {
+    // one of several frames in flight (rg_frames, bench.py): the heavy path sizes
+    // its grid for throughput (rg_kernels.hip launch_one, RgKernelArgs::pipelined)
+    return rg_launch_tiles(s, width, height, tiling, rgba_dev, rgb_dev, static_cast<hipStream_t>(stream), nullptr,
+                           nullptr, false, nullptr, 0, nullptr, 3, false, true);
 }
 
 }  // extern "C"
@@ -1158,7 +1193,8 @@ rg_status rg_render_image(const rg_scene *s, uint32_t width, uint32_t height, ui
 
 rg_status rg_host_register(void *ptr, size_t bytes) {
     if (!ptr || bytes == 0) return RG_ERR_INVALID_ARGUMENT;
-    if (!ok(hipHostRegister(ptr, bytes, hipHostRegisterDefault))) {
+    // portable: every device's DMA engine may write it (rg_render_multi's per-device copies)
+    if (!ok(hipHostRegister(ptr, bytes, hipHostRegisterPortable))) {
         (void)hipGetLastError();
         return RG_ERR_DEVICE;
     }
@@ -1285,7 +1321,7 @@ rg_status rg_debug_counters(const rg_scene *s, uint64_t out[16]) {
     if (!s || !out) return RG_ERR_INVALID_ARGUMENT;
     if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
     if (!ok(hipStreamSynchronize(s->last->stream)) ||
-        !ok(hipMemcpy(out, s->last->counters, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost)))
+        !ok(hipMemcpy(out, s->last->last_counters, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost)))
         return RG_ERR_DEVICE;
     return RG_OK;
 }
@@ -1303,13 +1339,17 @@ rg_status rg_trace(const rg_scene *s, const double *rays, uint32_t n, double *di
     if (!cx) st = RG_ERR_OUT_OF_MEMORY;
     RgKernelArgs a = rg_make_args(s);
     unsigned long long c[4] = {0, 0, 0, 0};
-    if (st == RG_OK) { s->last = cx; a.counters = cx->counters; }
+    // the trace kernel counts into the set the context's next render launch will
+    // use, and re-zeroes it after the read-back (that launch expects it zeroed)
+    unsigned long long *cs = cx ? cx->counters + (size_t)cx->cur * RG_COUNTER_WORDS : nullptr;
+    if (st == RG_OK) { s->last = cx; a.counters = cs; }
     if (st == RG_OK && (!ok(hipMemcpy(d_rays, rays, (size_t)n * 48, hipMemcpyHostToDevice)) ||
-                        !ok(hipMemset(cx->counters, 0, sizeof c)) ||
+                        !ok(hipMemset(cs, 0, sizeof c)) ||
                         !ok(rg_launch_trace(&a, (const double *)d_rays, n, (double *)d_dist, (int32_t *)d_body, nullptr)) ||
                         !ok(hipMemcpy(dist, d_dist, (size_t)n * 8, hipMemcpyDeviceToHost)) ||
                         !ok(hipMemcpy(body, d_body, (size_t)n * 4, hipMemcpyDeviceToHost)) ||
-                        !ok(hipMemcpy(c, cx->counters, sizeof c, hipMemcpyDeviceToHost))))
+                        !ok(hipMemcpy(c, cs, sizeof c, hipMemcpyDeviceToHost)) ||
+                        !ok(hipMemset(cs, 0, RG_COUNTER_WORDS * sizeof(unsigned long long)))))
         st = RG_ERR_DEVICE;
     if (d_rays) (void)hipFree(d_rays);
     if (d_dist) (void)hipFree(d_dist);

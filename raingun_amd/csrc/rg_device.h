@@ -133,6 +133,7 @@ struct RgKernelArgs {
     // frame
     uint32_t width, height;
     uint32_t tile_rows, tile_stride, tile_offset, out_rows;
+    uint32_t tile_base;      // the launch renders selected tiles tile_base, tile_base + 1, ... (output row 0 = its first row)
     double fov_adjustment;   // tan(fov.to_radians() / 2), ray.rs:45 (host libm)
     double aspect;           // width / height, ray.rs:43
     float def[3];            // scene.default_color
@@ -142,6 +143,7 @@ struct RgKernelArgs {
     float *rgb;              // nullable, out_rows * width * 3
     const uint32_t *tile_perm;     // nullable: dequeue order of the 8x8 tiles (expensive first)
     unsigned long long *counters;  // [0]=primary [1]=shadow [2]=secondary [3]=~error key [16+16q]=tile queue heads (RG_COUNTER_WORDS words)
+    unsigned long long *counters_next;  // nullable: the other counter set of the launch context, zeroed by the render kernel
     // frames of the shading tree for depths above the compiled arrays (rg_kernels.hip FrameStack<0>)
     void *deep_stack;        // grid threads x (max_depth - 1) frames, frame i of thread g at [i * deep_stride + g]
     uint32_t deep_stride;    // threads of the grid the buffer was sized for
@@ -168,6 +170,9 @@ struct RgKernelArgs {
     // 1: this launch is one of several frames in flight (rg_render_tiles_async):
     // the heavy path sizes its persistent grid for throughput, not latency (launch_one)
     uint32_t pipelined;
+    // (double)width, (double)height (ray.rs:46-51 divisions): kernel arguments land in SGPRs,
+    // where the kernel's own conversions would hold two loop-invariant VGPR pairs
+    double width_d, height_d;
 };
 
 __host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }

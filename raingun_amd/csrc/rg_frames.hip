@@ -17,6 +17,7 @@
 
 #include "../../include/raingun.h"
 #include "../../include/raingun_frames.h"
+#include "rg_internal.h"
 
 namespace {
 
@@ -143,8 +144,13 @@ void frames_release(rg_frames *f) {
     for (hipEvent_t e : f->rendered) (void)hipEventDestroy(e);
     for (hipEvent_t e : f->sent) (void)hipEventDestroy(e);
     for (hipEvent_t e : f->done) (void)hipEventDestroy(e);
+    rg_scene *sc = const_cast<rg_scene *>(f->scene);  // nullptr: the scene was destroyed first (it freed our launch state)
+    if (sc) {
+        auto &v = sc->frames;
+        v.erase(std::remove(v.begin(), v.end(), f), v.end());
+    }
     for (hipStream_t s : f->render) {
-        (void)rg_scene_release_stream(const_cast<rg_scene *>(f->scene), s);  // its launch state goes with it
+        if (sc) (void)rg_scene_release_stream(sc, s);  // its launch state goes with it
         (void)hipStreamDestroy(s);
     }
     if (f->comm_stream) (void)hipStreamDestroy(f->comm_stream);
@@ -153,6 +159,13 @@ void frames_release(rg_frames *f) {
 }
 
 }  // namespace
+
+void rg_frames_detach_scene(rg_frames *f) {
+    if (!f) return;
+    (void)hipSetDevice(f->device);
+    for (hipStream_t s : f->render) (void)hipStreamSynchronize(s);
+    f->scene = nullptr;
+}
 
 extern "C" {
 
@@ -215,6 +228,7 @@ rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t heigh
         frames_release(f);
         return RG_ERR_OUT_OF_MEMORY;
     }
+    scene->frames.push_back(f);
     *out = f;
     return RG_OK;
 }
@@ -222,12 +236,12 @@ rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t heigh
 void rg_frames_destroy(rg_frames *f) { frames_release(f); }
 
 rg_status rg_frames_step(rg_frames *f) {
-    if (!f) return RG_ERR_INVALID_ARGUMENT;
+    if (!f || !f->scene) return RG_ERR_INVALID_ARGUMENT;
     const int b = (int)(f->k % (unsigned long long)f->depth);
     hipStream_t rs = f->render[b];
     if (f->k >= (unsigned long long)f->depth && !ok(hipStreamWaitEvent(rs, f->done[b], 0))) return RG_ERR_DEVICE;
-    rg_status st = rg_render_tiles_async(f->scene, f->w, f->h, &f->tiling, static_cast<uint8_t *>(f->parts[b]),
-                                         nullptr, rs, nullptr);
+    rg_status st = rg_render_tiles_pipelined(f->scene, f->w, f->h, &f->tiling, static_cast<uint8_t *>(f->parts[b]),
+                                             nullptr, rs);
     if (st != RG_OK) return st;
     // off the root the part travels packed (3 B per pixel); the root's own part is read in place
     if (f->rank != 0 && !ok(rg_launch_pack_rgb(f->parts[b], f->packed[b], (size_t)f->slot_rows * f->w, rs)))
@@ -255,7 +269,7 @@ rg_status rg_frames_step(rg_frames *f) {
 }
 
 rg_status rg_frames_flush(rg_frames *f) {
-    if (!f) return RG_ERR_INVALID_ARGUMENT;
+    if (!f || !f->scene) return RG_ERR_INVALID_ARGUMENT;
     for (hipStream_t s : f->render) {
         if (!ok(hipStreamSynchronize(s))) return RG_ERR_DEVICE;
         // device errors of this rank's renders (the reference panics: rendering.rs, bodies.rs:324, scene.rs:38)

@@ -19,10 +19,31 @@
 // launches on one stream are ordered by the stream and reuse it.
 struct rg_launch_ctx {
     hipStream_t stream = nullptr;
-    unsigned long long *counters = nullptr;  // RG_COUNTER_WORDS words (rg_device.h), reset by every launch
+    // Two sets of RG_COUNTER_WORDS words (rg_device.h), used by alternate
+    // launches: a render kernel counts into set `cur` and zeroes the other set
+    // (the previous launch's, already read back: same stream), so the next
+    // launch finds its set zeroed without a memset of its own.
+    unsigned long long *counters = nullptr;
+    int cur = 0;
+    unsigned long long *last_counters = nullptr;  // the set of the latest launch (rg_debug_counters)
     unsigned long long *sticky = nullptr;    // first error of any launch since rg_stream_status cleared it
     uint32_t *tile_cost = nullptr, *tile_perm = nullptr;  // probe/sort scratch (rg_launch_tile_order), order
     size_t tile_cap = 0;
+    // the launch the cached tile_perm was made for: the order is a function of
+    // the frame geometry and the scene (probe rays, materials, lights, depth)
+    struct PermKey {
+        uint32_t width, height, tile_rows, tile_stride, tile_offset, tile_base, out_rows, tile_wlog, max_depth, n_lights;
+        double fov;
+        const void *mats;
+        bool operator==(const PermKey &o) const {
+            return width == o.width && height == o.height && tile_rows == o.tile_rows && tile_stride == o.tile_stride &&
+                   tile_offset == o.tile_offset && tile_base == o.tile_base && out_rows == o.out_rows &&
+                   tile_wlog == o.tile_wlog && max_depth == o.max_depth &&
+                   n_lights == o.n_lights && fov == o.fov && mats == o.mats;
+        }
+    };
+    bool perm_valid = false;
+    PermKey perm_key{};
     void *deep = nullptr;  // frames for depths above the compiled arrays (rg_kernels.hip FrameStack<0>)
     size_t deep_bytes = 0;
     double *prim = nullptr;  // sensor x per column then sensor y per row (RgKernelArgs::prim_sx / prim_sy)
@@ -107,6 +128,7 @@ struct rg_host_tables {
 };
 
 struct rg_multi_res;  // rg_multi.hip
+struct rg_frames;     // rg_frames.hip (include/raingun_frames.h)
 
 struct rg_scene {
     int device = 0;
@@ -140,12 +162,24 @@ struct rg_scene {
     int tile_order = -1;  // expensive tiles first (rg_kernels.hip "tile ordering"): -1 auto (heavy path), 0, 1
     int image_bands = 0;  // host-visible frames: 0 auto, -1 one launch writing host memory, 1..16 row bands
     int host_tile_wlog = RG_HOST_TILE_WLOG;  // tile shape of the one-launch host-visible path
+    // rg_render_multi (rg_debug_set_multi): 0 each device copies its rows to the host, 1 RCCL gather;
+    // stand-in: every "device" is this one, gathers through a stand-in (tests on one GPU);
+    // bands per device share in the direct mode (0: automatic)
+    int multi_mode = 0;
+    bool multi_stand_in = false;
+    int multi_bands = 0;
     std::shared_ptr<const rg_host_tables> host;
     mutable std::vector<rg_launch_ctx *> ctxs;  // one per stream used
     mutable rg_launch_ctx *last = nullptr;       // the context of the latest launch (rg_debug_counters)
     mutable rg_image_res img;
     mutable rg_multi_res *multi = nullptr;
+    // frame pipelines built on this scene: a scene destroyed first detaches them
+    // (rg_frames_destroy then no longer touches it), in either destruction order
+    mutable std::vector<rg_frames *> frames;
 };
+
+// rg_frames.hip: the scene of `f` is going away (rg_scene_destroy)
+void rg_frames_detach_scene(rg_frames *f);
 
 // Kernel arguments of a scene (tables, LDS arena, frame constants).
 RgKernelArgs rg_make_args(const rg_scene *s);
@@ -160,7 +194,10 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
                           rg_launch_ctx **ctx_out, bool timed = false, uint32_t *tile_flags = nullptr,
                           uint32_t frame_seq = 0, const uint32_t *cancel = nullptr, uint32_t tile_wlog = 3,
                           bool host_frame = false,   // host_frame: rgba_dev is page-locked host memory
-                          bool pipelined = false);   // frames in flight: size the grid for throughput
+                          bool pipelined = false,    // frames in flight: size the grid for throughput
+                          // a band of the tiling's selection: selected tiles [tile_first, tile_first + tile_count),
+                          // rgba_dev / rgb_dev pointing at tile_first's first row
+                          uint32_t tile_first = 0, uint32_t tile_count = 0xFFFFFFFFu);
 
 // Ray counts and status of a counter snapshot (stats nullable).
 rg_status rg_snap_status(const unsigned long long *snap, rg_stats *stats);

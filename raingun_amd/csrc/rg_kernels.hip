@@ -1218,7 +1218,7 @@ struct FrameStack<0> {
 
 __device__ __forceinline__ uint32_t out_row_to_y(const RgKernelArgs &a, uint32_t orow) {
     uint32_t tl = orow / a.tile_rows, r = orow - tl * a.tile_rows;
-    unsigned long long y = ((unsigned long long)tl * a.tile_stride + a.tile_offset) * a.tile_rows + r;
+    unsigned long long y = ((unsigned long long)(tl + a.tile_base) * a.tile_stride + a.tile_offset) * a.tile_rows + r;
     return y >= a.height ? 0xFFFFFFFFu : (uint32_t)y;
 }
 
@@ -1424,6 +1424,10 @@ template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH,
 __global__ __launch_bounds__(LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS, LB > 1 ? WPS : 1)
 void rg_render_kernel(RgKernelArgs a) {
     static_assert(!BVH || 4 * WPS <= RG_BVH_MAX_WAVES, "one BVH stack per wave");
+    // the launch context's other counter set (the previous launch's, read back
+    // already: same stream) starts the next launch at zero -- no memset per frame
+    if (blockIdx.x == 0 && a.counters_next)
+        for (uint32_t k = threadIdx.x; k < RG_COUNTER_WORDS; k += blockDim.x) a.counters_next[k] = 0ull;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     typename std::conditional<LSPH, SphLds, SphScalar>::type src;
     Cold T;
@@ -1493,6 +1497,13 @@ void rg_render_kernel(RgKernelArgs a) {
     constexpr bool HOSTF = MAXD == 0;
     __shared__ uint32_t tile_px[HOSTF ? (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) : 1][64];
     uint32_t *my_px = &tile_px[HOSTF ? threadIdx.x >> 6 : 0][lane];
+    // Light path: a diffuse hit's shading factors wait in LDS while its shadow
+    // batch is traced (field k of the lane at park[k][lane], conflict-free), so
+    // that only the query's own state is held in VGPRs across the trace.
+    constexpr int PK_PP = 0, PK_LIN = LB, PK_REFL = 2 * LB, PK_COL = 2 * LB + 1, PK_KIND = 2 * LB + 4,
+                  PK_R = 2 * LB + 5, PK_N = 2 * LB + 6;
+    __shared__ float park_lds[LB > 1 ? RG_LIGHT_BLOCK_WAVES : 1][LB > 1 ? PK_N : 1][64];
+    float *park = &park_lds[LB > 1 ? (threadIdx.x >> 6) % RG_LIGHT_BLOCK_WAVES : 0][0][lane];  // field k at park[64 k]
 #ifdef RG_BVH_STATS
     if (lane < 16) rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][lane] = 0ull;
 #endif
@@ -1525,7 +1536,6 @@ void rg_render_kernel(RgKernelArgs a) {
     Ray q;                 // current query (shadow: q.o = shared origin)
     ShadowBatch<LB> sb;        // shadow: the batch's directions and light distances
     uint32_t occl_full = 0u;
-    float pp[LB], lin[LB], refl_f = 0.0f;  // light path: per-light max(n.l, 0), intensity; albedo/pi
     int qdepth = 0;        // closest: depth of the ray
     // hit being shaded
     V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0), hd = v3(0, 0, 0);
@@ -1571,7 +1581,7 @@ void rg_render_kernel(RgKernelArgs a) {
             bool unwind = false;
             bool shade = false;           // run a shade_diffuse step this iteration
             const int rmode = mode;       // kind of result the lane holds
-            if (rmode == MODE_WAIT) {
+            if (TASKS && rmode == MODE_WAIT) {
                 unwind = true;  // poll the awaited subtree (top frame FR_REFR_WAIT)
             } else if (rmode == MODE_CLOSEST) {
                 if (c.nan && c.nhit >= 2) raise_error(a, pixel, RG_ERR_NAN_DISTANCE);
@@ -1586,43 +1596,50 @@ void rg_render_kernel(RgKernelArgs a) {
                     V3 n;
                     if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
                     if (m.surface != RG_SURFACE_REFRACTIVE) {
-                        bcol = surface_color(T.texs, m, b, h);
-                        hb = c.id; hdepth = qdepth;
                         if constexpr (LB > 1) {
                             // ONE batch covers every light (n_lights <= LB on this path): set it
-                            // up now, with the per-light shading factors, so that no hit-point
-                            // state (h, n, incident) has to survive the shadow pass
-                            refl_f = m.albedo / PI_F;                               // rendering.rs:164
+                            // up now, with the per-light shading factors (parked in LDS), so that
+                            // no hit-point state (h, n, incident) has to survive the shadow pass
+                            const C3 col = surface_color(T.texs, m, b, h);
+                            park[64 * PK_COL] = col.r; park[64 * (PK_COL + 1)] = col.g; park[64 * (PK_COL + 2)] = col.b;
+                            park[64 * PK_REFL] = m.albedo / PI_F;                   // rendering.rs:164
+                            // how the batch's colour is used: 0 diffuse, 1 reflecting at the depth
+                            // limit (mix with the default colour), 2 reflecting with a frame
+                            const int kind = m.surface == RG_SURFACE_DIFFUSE ? 0 : qdepth + 1 < max_depth ? 2 : 1;
+                            park[64 * PK_KIND] = __int_as_float(kind);
+                            park[64 * PK_R] = m.reflectivity;
+                            // the shadow rays' origin hit + n*bias (rendering.rs:148) is also the
+                            // reflection ray's origin (ray.rs:57): q.o serves both, and q.d (unused
+                            // by the shadow pass) carries the reflection direction until the
+                            // batch is shaded -- the frame holds only colour state
+                            q.o = add(h, scl(n, SHADOW_BIAS));
                             if (m.surface == RG_SURFACE_REFLECTING && qdepth + 1 < max_depth) {
-                                Frame &f = stk[sp++];                               // reflection ray of
-                                const Ray rr = reflection(n, q.d, h);               // rendering.rs:88,
+                                Frame &f = stk[sp++];                               // rendering.rs:88,
                                 f.type = FR_REFL_PEND;                              // D filled in later
-                                f.rr[0] = rr.o.x; f.rr[1] = rr.o.y; f.rr[2] = rr.o.z;
-                                f.rr[3] = rr.d.x; f.rr[4] = rr.d.y; f.rr[5] = rr.d.z;
                                 f.f[3] = m.reflectivity;
                                 f.cdepth = qdepth + 1;
+                                q.d = sub(q.d, scl(n, 2.0 * dot(q.d, n)));          // ray.rs:58
                             }
-                            q.o = add(h, scl(n, SHADOW_BIAS));                      // rendering.rs:148
                             occl_full = 0u;
 #pragma unroll
                             for (int l = 0; l < LB; ++l) {
                                 if (l < a.n_lights) {
                                     const RgLightDev L = T.lights[l];
                                     light_dir_dist(L, h, sb.d[l], sb.ld[l]);
-                                    pp[l] = fmaxf((float)dot(n, sb.d[l]), 0.0f);    // rendering.rs:161-162
-                                    lin[l] = light_intensity(L, h);                 // pure; used if lit
+                                    park[64 * (PK_PP + l)] = fmaxf((float)dot(n, sb.d[l]), 0.0f);  // rendering.rs:161-162
+                                    park[64 * (PK_LIN + l)] = light_intensity(L, h);               // pure; used if lit
                                     occl_full |= 1u << l;
                                     n_shadow++;
                                 } else {
                                     sb.d[l] = v3(0.0, 0.0, 1.0);
                                     sb.ld[l] = 0.0;
-                                    pp[l] = 0.0f;
-                                    lin[l] = 0.0f;
                                 }
                             }
                             if (a.n_lights > 0) mode = MODE_SHADOW;
                             else shade = true;  // no lights: finish with black (rendering.rs:138)
                         } else {
+                            bcol = surface_color(T.texs, m, b, h);
+                            hb = c.id; hdepth = qdepth;
                             fin = c3(0.0f, 0.0f, 0.0f);
                             hp = h; hn = n; hd = q.d; li = 0;
                             shade = true;
@@ -1630,50 +1647,60 @@ void rg_render_kernel(RgKernelArgs a) {
                     } else {
                         float kr = (float)fresnel(q.d, n, m.index);
                         C3 surf = surface_color(T.texs, m, b, h);
-                        Ray rr = reflection(n, q.d, h);
                         int cd = qdepth + 1;
-                        C3 tc = def;
-                        bool trace_t = false;
-                        Ray tr;
-                        if (kr < 1.0f) {
-                            if (!transmission(n, q.d, h, m.index, tr)) raise_error(a, pixel, RG_ERR_TRANSMISSION);
-                            else if (cd < max_depth) trace_t = true;
-                        }
                         if (cd >= max_depth) {
-                            C3 col = cadd(cscl(def, kr), cscl(tc, 1.0f - kr));
+                            // the transmission ray's unwrap (rendering.rs:106) precedes cast_ray's depth test
+                            Ray tr;
+                            if (kr < 1.0f && !transmission(n, q.d, h, m.index, tr)) raise_error(a, pixel, RG_ERR_TRANSMISSION);
+                            C3 col = cadd(cscl(def, kr), cscl(def, 1.0f - kr));
                             ret = cmul(cscl(col, m.transparency), surf);
                             unwind = true;
                         } else {
                             Frame &f = stk[sp++];
                             f.f[0] = kr; f.f[1] = m.transparency;
                             f.f[2] = surf.r; f.f[3] = surf.g; f.f[4] = surf.b;
-                            f.f[5] = tc.r; f.f[6] = tc.g; f.f[7] = tc.b;
                             f.cdepth = cd;
-                            if (trace_t) {
-                                // the reflection subtree waits until the transmission subtree is
-                                // done: publish it, so an idle lane of the block can trace it now
-                                int slot = -1;
+                            // rendering.rs:100-113: the transmission subtree is traced first while
+                            // the reflection ray (ray.rs:56-60) waits in the frame or, with task
+                            // splitting, is published so an idle lane of the block can trace it now
+                            bool trace_t = false;
+                            if (kr < 1.0f) {
                                 if constexpr (TASKS) {
-                                    slot = pool_alloc(lane);
-                                    if (slot >= 0) {
-                                        double *pr = rg_pool.ray[slot];
-                                        pr[0] = rr.o.x; pr[1] = rr.o.y; pr[2] = rr.o.z;
-                                        pr[3] = rr.d.x; pr[4] = rr.d.y; pr[5] = rr.d.z;
-                                        rg_pool.depth[slot] = cd;
-                                        rg_pool.pix[slot] = pixel;
-                                        pool_publish(slot);
-                                        f.type = FR_REFR_TASK | (slot << 8);
+                                    Ray tr;
+                                    if (transmission(n, q.d, h, m.index, tr)) {
+                                        trace_t = true;
+                                        const Ray rr = reflection(n, q.d, h);
+                                        const int slot = pool_alloc(lane);
+                                        if (slot >= 0) {
+                                            double *pr = rg_pool.ray[slot];
+                                            pr[0] = rr.o.x; pr[1] = rr.o.y; pr[2] = rr.o.z;
+                                            pr[3] = rr.d.x; pr[4] = rr.d.y; pr[5] = rr.d.z;
+                                            rg_pool.depth[slot] = cd;
+                                            rg_pool.pix[slot] = pixel;
+                                            pool_publish(slot);
+                                            f.type = FR_REFR_TASK | (slot << 8);
+                                        } else {
+                                            f.type = FR_REFR_T;
+                                            f.rr[0] = rr.o.x; f.rr[1] = rr.o.y; f.rr[2] = rr.o.z;
+                                            f.rr[3] = rr.d.x; f.rr[4] = rr.d.y; f.rr[5] = rr.d.z;
+                                        }
+                                        q = tr;
                                     }
-                                }
-                                if (slot < 0) {
-                                    f.type = FR_REFR_T;
+                                } else {
+                                    // the reflection ray goes to the frame BEFORE the transmission ray
+                                    // is built (into q, written only on success): fewer live values
+                                    const Ray rr = reflection(n, q.d, h);
                                     f.rr[0] = rr.o.x; f.rr[1] = rr.o.y; f.rr[2] = rr.o.z;
                                     f.rr[3] = rr.d.x; f.rr[4] = rr.d.y; f.rr[5] = rr.d.z;
+                                    f.type = FR_REFR_T;
+                                    trace_t = transmission(n, q.d, h, m.index, q);
                                 }
-                                q = tr;
-                            } else {
+                                if (!trace_t) raise_error(a, pixel, RG_ERR_TRANSMISSION);
+                            }
+                            if (!trace_t) {  // kr >= 1 (or the transmission panic): refraction colour = default
                                 f.type = FR_REFR_R;
-                                q = rr;
+                                f.f[5] = def.r; f.f[6] = def.g; f.f[7] = def.b;
+                                q = reflection(n, q.d, h);
                             }
                             qdepth = cd;
                             mode = MODE_CLOSEST;
@@ -1687,35 +1714,35 @@ void rg_render_kernel(RgKernelArgs a) {
             if constexpr (LB > 1) {
               if (shade) {
                 // shade_diffuse accumulation over the batch (rendering.rs:141-170), in light order
-                const RgMatDev m = T.mats[hb];
+                const C3 bc = c3(park[64 * PK_COL], park[64 * (PK_COL + 1)], park[64 * (PK_COL + 2)]);
+                const float refl = park[64 * PK_REFL];
                 C3 acc = c3(0.0f, 0.0f, 0.0f);
 #pragma unroll
                 for (int l = 0; l < LB; ++l) {
                     if (l < a.n_lights) {
                         const RgLightDev L = T.lights[l];
-                        const float inten = !((occl >> l) & 1u) ? lin[l] : 0.0f;
-                        const float power = pp[l] * inten;
-                        C3 lc = cscl(cscl(c3(L.color[0], L.color[1], L.color[2]), power), refl_f);
-                        acc = cadd(acc, cmul(bcol, lc));
+                        const float inten = !((occl >> l) & 1u) ? park[64 * (PK_LIN + l)] : 0.0f;
+                        const float power = park[64 * (PK_PP + l)] * inten;
+                        C3 lc = cscl(cscl(c3(L.color[0], L.color[1], L.color[2]), power), refl);
+                        acc = cadd(acc, cmul(bc, lc));
                     }
                 }
                 C3 dcol = cclamp(acc);
-                if (m.surface == RG_SURFACE_DIFFUSE) {
+                const int kind = __float_as_int(park[64 * PK_KIND]);
+                if (kind == 0) {  // Diffuse
                     ret = dcol;
                     unwind = true;
                 } else {  // Reflecting (rendering.rs:86-91)
-                    const float r = m.reflectivity;
-                    const int cd = hdepth + 1;
-                    if (cd >= max_depth) {
+                    if (kind == 1) {  // the reflection ray would be at depth >= max (rendering.rs:123-124)
+                        const float r = park[64 * PK_R];
                         ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
                         unwind = true;
                     } else {
                         Frame &f = stk[sp - 1];  // the FR_REFL_PEND pushed at the hit
                         f.type = FR_REFL;
                         f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b;
-                        q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
-                        q.d = v3(f.rr[3], f.rr[4], f.rr[5]);
-                        qdepth = cd;
+                        // q = the reflection ray (origin = the shadow origin, direction set at the hit)
+                        qdepth = f.cdepth;
                         mode = MODE_CLOSEST;
                         n_sec++;
                     }
@@ -1951,8 +1978,8 @@ void rg_render_kernel(RgKernelArgs a) {
                         sx = a.prim_sx[x];
                         sy = a.prim_sy[y];
                     } else {
-                        sx = ((((double)x + 0.5) / (double)a.width) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
-                        sy = (1.0 - (((double)y + 0.5) / (double)a.height) * 2.0) * a.fov_adjustment;
+                        sx = ((((double)x + 0.5) / a.width_d) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
+                        sy = (1.0 - (((double)y + 0.5) / a.height_d) * 2.0) * a.fov_adjustment;
                     }
                     q.o = v3(0.0, 0.0, 0.0);
                     q.d = normalize(v3(sx, sy, -1.0));
@@ -2487,6 +2514,9 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
     // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
     const bool heavy = rg_heavy_path(*a);
     if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream, gt);
+#ifdef RG_DEV_LIGHT_ONLY  // development builds: resource reports of the light kernels only
+    return hipErrorNotSupported;
+#else
     const unsigned long long tiles = rg_tile_count(*a);
     // frames in flight (pipelined): the throughput-sized grid already keeps blocks long;
     // task splitting then costs more than it saves (1/8 share 0.400 -> 0.384 ms without:
@@ -2497,6 +2527,7 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
                      : launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, false>(a, stream, gt);
     return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, true>(a, stream, gt)
                  : launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, false>(a, stream, gt);
+#endif
 }
 
 // Frame-stack capacity of each compiled array instantiation; deeper scenes use
@@ -2504,10 +2535,14 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
 extern "C" int rg_max_array_frames(void) { return 64; }
 
 static hipError_t dispatch_depth(const RgKernelArgs *a, int maxd, hipStream_t stream, size_t *gt) {
+#ifdef RG_DEV_ONE_DEPTH  // development builds: the MAXD = 8 instantiations only
+    return maxd <= 8 ? launch_depth<8>(a, stream, gt) : hipErrorNotSupported;
+#else
     if (maxd <= 8) return launch_depth<8>(a, stream, gt);
     if (maxd <= 16) return launch_depth<16>(a, stream, gt);
     if (maxd <= 64) return launch_depth<64>(a, stream, gt);
     return launch_depth<0>(a, stream, gt);
+#endif
 }
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream) {

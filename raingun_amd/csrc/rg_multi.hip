@@ -2,8 +2,19 @@
 // §8(b), §5: "rg_render_multi ... ncclCommInitAll").
 //
 // The frame is cut into tile_rows-row tiles dealt round-robin (tile t ->
-// device t % N, the balance argument of DESIGN.md §6).  Per call:
-//   device i, stream i : render its tiles into part[i] (its replica of the scene)
+// device t % N, the balance argument of DESIGN.md §6); each device renders its
+// tiles with its own replica of the scene.  The frame must end in HOST memory
+// (rendering.rs:24-38 returns an ImageBuffer), and each device has its own
+// PCIe link, so by default the devices deliver their own rows (DIRECT):
+//   device i, render streams : its tiles in K bands (two streams, alternating)
+//   device i, copy stream    : after band b, ONE strided copy (hipMemcpy2DAsync)
+//                              of the band's tiles straight to their image rows
+//                              in page-locked host memory (the caller's buffer,
+//                              or a pinned frame fed to a pageable buffer band by
+//                              band by host threads)
+// -- N links carry 1/N of the frame each, overlapped with the later bands'
+// renders.  The RCCL path (GATHER, rg_debug_set_multi mode 1) keeps the
+// collective design of SURVEY.md §8(e):
 //   all devices        : ONE ncclGather of the equal-size parts to device 0, packed to
 //                        RGB (3 B per pixel: alpha is always 255) off device 0
 //                        (ncclGroupStart/End: one thread issues N ranks' calls)
@@ -11,6 +22,12 @@
 //                        copy the frame to the caller's host buffer
 // RCCL is loaded with dlopen, so libraingun_hip.so links no collective
 // library and shares the one already in a process (PyTorch's) if there is one.
+//
+// Stand-in (rg_debug_set_multi stand_in = 1, for tests on one GPU): every
+// "device" is the scene's device, each with its own replica, and the gather
+// goes through a stand-in with ncclGather's signature and group semantics
+// (device copies into the root's receive buffer, ordered after each rank's
+// render) -- so every N > 1 code path runs on a single GPU.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <link.h>
@@ -24,6 +41,7 @@
 #include <vector>
 
 #include "../../include/raingun.h"
+#include "../../include/raingun_debug.h"
 #include "rg_internal.h"
 
 // rg_frames.hip: parts travel as packed RGB (3 B per pixel); device 0 reads its own part in place
@@ -93,22 +111,68 @@ const Rccl *rccl() {
 constexpr int kNcclUint8 = 1;       // ncclDataType_t (rccl.h)
 constexpr int kNcclInProgress = 7;  // a non-blocking communicator's "enqueued"
 
+// ---------------------------------------------------------------- stand-in gather
+// ncclGather's signature and the semantics rg_render_multi relies on: within
+// one group the root (rank 0) is called first with the receive buffer; rank
+// r's `count` bytes land at recv + r * count once rank r's earlier work on its
+// stream is done, and the root's stream is ordered after every copy.
+struct StandInGroup {
+    void *root_recv = nullptr;
+    hipStream_t root_stream = nullptr;
+    std::vector<hipEvent_t> ev;  // one per rank
+};
+struct StandInComm {
+    int rank = 0;
+    StandInGroup *g = nullptr;
+};
+
+int stand_in_gather(const void *send, void *recv, size_t count, int dtype, int root, void *comm, hipStream_t stream) {
+    StandInComm *c = static_cast<StandInComm *>(comm);
+    if (!c || dtype != kNcclUint8 || root != 0) return 1;
+    StandInGroup *g = c->g;
+    if (c->rank == 0) {
+        if (!recv) return 1;
+        g->root_recv = recv;
+        g->root_stream = stream;
+        return ok(hipMemcpyAsync(recv, send, count, hipMemcpyDeviceToDevice, stream)) ? 0 : 1;
+    }
+    if (!g->root_recv || c->rank >= (int)g->ev.size()) return 1;
+    hipEvent_t e = g->ev[c->rank];
+    if (!ok(hipEventRecord(e, stream)) || !ok(hipStreamWaitEvent(g->root_stream, e, 0))) return 1;
+    return ok(hipMemcpyAsync(static_cast<char *>(g->root_recv) + (size_t)c->rank * count, send, count,
+                             hipMemcpyDeviceToDevice, g->root_stream))
+               ? 0
+               : 1;
+}
+
+#ifndef RG_MULTI_BAND_PX
+#define RG_MULTI_BAND_PX (1u << 20)  // a device's share is cut into bands of about this many pixels (at most 4)
+#endif
+
 }  // namespace
 
-// Per-scene multi-GPU state for one (ngpus, width, height, tile_rows).
+// Per-scene multi-GPU state for one (ngpus, width, height, tile_rows, mode).
 struct rg_multi_res {
     int n = 0;
     uint32_t w = 0, h = 0, T = 0, slot_rows = 0;
+    int mode = 0;            // 0: direct per-device copies to the host, 1: RCCL gather
+    bool stand_in = false;
     size_t part_bytes = 0;   // RGBA part
-    size_t slot_bytes = 0;   // packed RGB part each device sends
+    size_t slot_bytes = 0;   // packed RGB part each device sends (gather)
     std::vector<int> devs;
     std::vector<rg_scene *> reps;      // reps[0] = the scene itself (not owned)
     std::vector<void *> comms;
-    std::vector<hipStream_t> streams;
+    std::vector<StandInComm> sic;      // stand-in communicators
+    StandInGroup sig;
+    std::vector<hipStream_t> streams;  // render stream A per device (gather: the only one)
+    std::vector<hipStream_t> streams2; // direct: render stream B per device (bands alternate)
+    std::vector<hipStream_t> copies;   // direct: device-to-host copy stream per device
+    std::vector<std::vector<hipEvent_t>> ev_band, ev_copy;  // direct: per device, per band
     std::vector<void *> parts, packed;            // packed[0] unused: device 0's part is read in place
-    void *gathered = nullptr, *image = nullptr;  // device 0
-    unsigned long long *snap = nullptr;          // pinned: 4 words per device
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;     // device 0: render start .. frame assembled
+    void *gathered = nullptr, *image = nullptr;  // device 0 (gather)
+    void *h_frame = nullptr;                     // direct into pageable memory: pinned, portable frame
+    unsigned long long *snap = nullptr;          // pinned: 4 words per (device, band)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;     // device 0: render start .. its last band / frame assembled
 };
 
 namespace {
@@ -118,14 +182,25 @@ void free_res(rg_multi_res *m) {
     const Rccl *r = g_rccl.handle ? &g_rccl : nullptr;
     for (int i = 0; i < (int)m->devs.size(); ++i) {
         (void)hipSetDevice(m->devs[i]);
-        if (i < (int)m->streams.size() && m->streams[i]) (void)hipStreamSynchronize(m->streams[i]);
+        for (auto *v : {&m->streams, &m->streams2, &m->copies})
+            if (i < (int)v->size() && (*v)[i]) (void)hipStreamSynchronize((*v)[i]);
     }
     for (int i = 0; i < (int)m->devs.size(); ++i) {
         (void)hipSetDevice(m->devs[i]);
-        if (i < (int)m->comms.size() && m->comms[i] && r) (void)r->destroy(m->comms[i]);
+        if (!m->stand_in && i < (int)m->comms.size() && m->comms[i] && r) (void)r->destroy(m->comms[i]);
         if (i < (int)m->parts.size() && m->parts[i]) (void)hipFree(m->parts[i]);
         if (i < (int)m->packed.size() && m->packed[i]) (void)hipFree(m->packed[i]);
-        if (i < (int)m->streams.size() && m->streams[i]) (void)hipStreamDestroy(m->streams[i]);
+        // the render streams' launch state lives in the replicas; the scene's own
+        // (reps[0]) outlives these streams, so forget it before they go
+        for (auto *v : {&m->streams, &m->streams2}) {
+            if (i >= (int)v->size() || !(*v)[i]) continue;
+            if (i < (int)m->reps.size() && m->reps[i]) (void)rg_scene_release_stream(m->reps[i], (*v)[i]);
+            (void)hipStreamDestroy((*v)[i]);
+        }
+        if (i < (int)m->copies.size() && m->copies[i]) (void)hipStreamDestroy(m->copies[i]);
+        for (auto *v : {&m->ev_band, &m->ev_copy})
+            if (i < (int)v->size())
+                for (hipEvent_t e : (*v)[i]) if (e) (void)hipEventDestroy(e);
         if (i > 0 && i < (int)m->reps.size() && m->reps[i]) rg_scene_free(m->reps[i]);
     }
     if (!m->devs.empty()) {
@@ -134,61 +209,256 @@ void free_res(rg_multi_res *m) {
         if (m->image) (void)hipFree(m->image);
         if (m->ev0) (void)hipEventDestroy(m->ev0);
         if (m->ev1) (void)hipEventDestroy(m->ev1);
+        for (hipEvent_t e : m->sig.ev) if (e) (void)hipEventDestroy(e);
     }
     if (m->snap) (void)hipHostFree(m->snap);
+    if (m->h_frame) (void)hipHostFree(m->h_frame);
     delete m;
+}
+
+constexpr int kMaxBands = 4;
+
+// Bands of a device's share (direct mode): K bands of J selected tiles each.
+int multi_bands(const rg_scene *s, uint32_t W, uint32_t H, int n) {
+    if (s->multi_bands > 0) return std::min(s->multi_bands, kMaxBands);
+    const size_t share = ((size_t)W * H + (size_t)n - 1) / (size_t)n;
+    return (int)std::max<size_t>(1, std::min<size_t>(kMaxBands, share / RG_MULTI_BAND_PX));
 }
 
 rg_status build_res(const rg_scene *s, int n, uint32_t W, uint32_t H, uint32_t T, rg_multi_res **out) {
     *out = nullptr;
-    const Rccl *r = rccl();
-    if (!r) return RG_ERR_COLLECTIVE;
+    const bool stand_in = s->multi_stand_in;
+    const int mode = s->multi_mode;
+    const Rccl *r = nullptr;
+    if (mode == 1 && !stand_in && !(r = rccl())) return RG_ERR_COLLECTIVE;
     int ndev = 0;
-    if (!ok(hipGetDeviceCount(&ndev)) || n > ndev) return RG_ERR_INVALID_ARGUMENT;
+    if (!ok(hipGetDeviceCount(&ndev)) || (!stand_in && n > ndev) || n > 64) return RG_ERR_INVALID_ARGUMENT;
     rg_multi_res *m = new (std::nothrow) rg_multi_res();
     if (!m) return RG_ERR_OUT_OF_MEMORY;
     m->n = n;
     m->w = W;
     m->h = H;
     m->T = T;
+    m->mode = mode;
+    m->stand_in = stand_in;
     const uint32_t tiles = (H + T - 1) / T;
     m->slot_rows = (tiles + (uint32_t)n - 1) / (uint32_t)n * T;  // equal on every device
     m->part_bytes = (size_t)m->slot_rows * W * 4;
     m->slot_bytes = rg_packed_slot_bytes(m->slot_rows, W);
-    for (int i = 0; i < n; ++i) m->devs.push_back((s->device + i) % ndev);
+    for (int i = 0; i < n; ++i) m->devs.push_back(stand_in ? s->device : (s->device + i) % ndev);
     m->reps.assign(n, nullptr);
     m->comms.assign(n, nullptr);
     m->streams.assign(n, nullptr);
     m->parts.assign(n, nullptr);
     m->packed.assign(n, nullptr);
+    if (mode == 0) {
+        m->streams2.assign(n, nullptr);
+        m->copies.assign(n, nullptr);
+        m->ev_band.assign(n, std::vector<hipEvent_t>(kMaxBands, nullptr));
+        m->ev_copy.assign(n, std::vector<hipEvent_t>(kMaxBands, nullptr));
+    }
     m->reps[0] = const_cast<rg_scene *>(s);
     rg_status st = RG_OK;
     for (int i = 1; i < n && st == RG_OK; ++i) st = rg_scene_replica(s, m->devs[i], &m->reps[i]);
+    auto mk_stream = [](hipStream_t &x) { return ok(hipStreamCreateWithFlags(&x, hipStreamNonBlocking)); };
     for (int i = 0; i < n && st == RG_OK; ++i) {
-        if (!ok(hipSetDevice(m->devs[i])) || !ok(hipStreamCreateWithFlags(&m->streams[i], hipStreamNonBlocking)))
+        if (!ok(hipSetDevice(m->devs[i])) || !mk_stream(m->streams[i]))
             st = RG_ERR_DEVICE;
         else if (!ok(hipMalloc(&m->parts[i], std::max(m->part_bytes, m->slot_bytes))) ||
                  !ok(hipMemset(m->parts[i], 0, std::max(m->part_bytes, m->slot_bytes))) ||
-                 (i > 0 && !ok(hipMalloc(&m->packed[i], m->slot_bytes))))
+                 (mode == 1 && i > 0 && !ok(hipMalloc(&m->packed[i], m->slot_bytes))))
             st = RG_ERR_OUT_OF_MEMORY;  // padding rows of the last tiles stay zero
+        if (st == RG_OK && mode == 0) {
+            if (!mk_stream(m->streams2[i]) || !mk_stream(m->copies[i])) st = RG_ERR_DEVICE;
+            for (int b = 0; b < kMaxBands && st == RG_OK; ++b)
+                if (!ok(hipEventCreateWithFlags(&m->ev_band[i][b], hipEventDisableTiming)) ||
+                    !ok(hipEventCreateWithFlags(&m->ev_copy[i][b], hipEventDisableTiming)))
+                    st = RG_ERR_DEVICE;
+        }
     }
     if (st == RG_OK) {
         void *snap = nullptr;
         (void)hipSetDevice(m->devs[0]);
-        if (!ok(hipMalloc(&m->gathered, m->slot_bytes * (size_t)n)) || !ok(hipMalloc(&m->image, (size_t)H * W * 4)) ||
-            !ok(hipHostMalloc(&snap, (size_t)n * 4 * sizeof(unsigned long long), hipHostMallocPortable)))
+        if ((mode == 1 && (!ok(hipMalloc(&m->gathered, m->slot_bytes * (size_t)n)) ||
+                           !ok(hipMalloc(&m->image, (size_t)H * W * 4)))) ||
+            !ok(hipHostMalloc(&snap, (size_t)n * kMaxBands * 4 * sizeof(unsigned long long), hipHostMallocPortable)))
             st = RG_ERR_OUT_OF_MEMORY;
         m->snap = static_cast<unsigned long long *>(snap);
         if (st == RG_OK && (!ok(hipEventCreate(&m->ev0)) || !ok(hipEventCreate(&m->ev1)))) st = RG_ERR_DEVICE;
     }
-    if (st == RG_OK && r->init_all(m->comms.data(), n, m->devs.data()) != 0) st = RG_ERR_COLLECTIVE;
+    if (st == RG_OK && mode == 1) {
+        if (stand_in) {
+            m->sic.resize(n);
+            m->sig.ev.assign(n, nullptr);
+            for (int i = 0; i < n && st == RG_OK; ++i) {
+                m->sic[i] = StandInComm{i, &m->sig};
+                m->comms[i] = &m->sic[i];
+                if (!ok(hipEventCreateWithFlags(&m->sig.ev[i], hipEventDisableTiming))) st = RG_ERR_DEVICE;
+            }
+        } else if (r->init_all(m->comms.data(), n, m->devs.data()) != 0) {
+            for (void *&c : m->comms) c = nullptr;  // not (fully) created
+            st = RG_ERR_COLLECTIVE;
+        }
+    }
     if (st != RG_OK) {
-        for (void *&c : m->comms) c = nullptr;  // not (fully) created
         free_res(m);
         return st;
     }
     *out = m;
     return RG_OK;
+}
+
+// Stats of all (device, band) launches: rays summed, the lowest erroring pixel.
+rg_status merge_snaps(const rg_multi_res *m, int per_dev, rg_stats *stats) {
+    rg_stats total;
+    std::memset(&total, 0, sizeof total);
+    unsigned long long worst = 0;  // complemented keys: the max is the lowest erroring pixel
+    for (int k = 0; k < m->n * per_dev; ++k) {
+        total.rays.primary += m->snap[4 * k];
+        total.rays.shadow += m->snap[4 * k + 1];
+        total.rays.secondary += m->snap[4 * k + 2];
+        worst = std::max(worst, m->snap[4 * k + 3]);
+    }
+    unsigned long long w4[4] = {0, 0, 0, worst};
+    rg_stats es;
+    const rg_status err = rg_snap_status(w4, &es);
+    total.error_pixel = es.error_pixel;
+    float ms = 0.0f;
+    (void)hipSetDevice(m->devs[0]);
+    (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
+    total.kernel_ms = ms;
+    if (stats) *stats = total;
+    return err;
+}
+
+// RCCL path: render, ONE grouped gather to device 0, re-interleave, one copy to the host.
+rg_status render_gather(const rg_scene *s, rg_multi_res *m, uint8_t *rgba_out, rg_stats *stats) {
+    const uint32_t W = m->w, H = m->h, T = m->T;
+    const int n = m->n;
+    if (!ok(hipSetDevice(m->devs[0])) || !ok(hipEventRecord(m->ev0, m->streams[0]))) return RG_ERR_DEVICE;
+    for (int i = 0; i < n; ++i) {
+        const rg_tiling t = {T, (uint32_t)n, (uint32_t)i};
+        rg_status st = rg_launch_tiles(m->reps[i], W, H, &t, static_cast<uint8_t *>(m->parts[i]), nullptr,
+                                       m->streams[i], m->snap + 4 * i, nullptr);
+        if (st != RG_OK) return st;
+        if (i > 0 && !ok(rg_launch_pack_rgb(m->parts[i], m->packed[i], (size_t)m->slot_rows * W, m->streams[i])))
+            return RG_ERR_DEVICE;
+    }
+    // one gather of the equal-size parts to device 0 (all ranks' calls in one group)
+    const Rccl *r = m->stand_in ? nullptr : rccl();
+    const pfn_gather gather = m->stand_in ? stand_in_gather : r->gather;
+    if (r && r->group_start() != 0) return RG_ERR_COLLECTIVE;
+    int gerr = 0;
+    for (int i = 0; i < n; ++i) {
+        (void)hipSetDevice(m->devs[i]);
+        const int g = gather(i == 0 ? m->parts[i] : m->packed[i], i == 0 ? m->gathered : nullptr, m->slot_bytes,
+                             kNcclUint8, 0, m->comms[i], m->streams[i]);
+        if (g != 0 && g != kNcclInProgress && gerr == 0) gerr = g;
+    }
+    const int ge = r ? r->group_end() : 0;
+    if (gerr != 0 || (ge != 0 && ge != kNcclInProgress)) return RG_ERR_COLLECTIVE;
+    // device 0: re-interleave, copy to the host
+    if (!ok(hipSetDevice(m->devs[0])) ||
+        !ok(rg_launch_reinterleave(m->gathered, m->parts[0], m->image, W, H, T, (uint32_t)n, m->slot_bytes,
+                                   m->streams[0])) ||
+        !ok(hipEventRecord(m->ev1, m->streams[0])) ||
+        !ok(hipMemcpyAsync(rgba_out, m->image, (size_t)H * W * 4, hipMemcpyDeviceToHost, m->streams[0])))
+        return RG_ERR_DEVICE;
+    for (int i = n - 1; i >= 0; --i)
+        if (!ok(hipSetDevice(m->devs[i])) || !ok(hipStreamSynchronize(m->streams[i]))) return RG_ERR_DEVICE;
+    return merge_snaps(m, 1, stats);
+}
+
+// Direct path: every device renders its tiles in K bands and copies each band
+// straight to its image rows in page-locked host memory over its own link.
+rg_status render_direct(const rg_scene *s, rg_multi_res *m, uint8_t *rgba_out, rg_stats *stats) {
+    const uint32_t W = m->w, H = m->h, T = m->T;
+    const int n = m->n;
+    const size_t row4 = (size_t)W * 4, frame_bytes = (size_t)H * row4;
+    // destination: the caller's buffer if page-locked, else the pinned frame
+    uint8_t *dst = rg_host_is_pinned(rgba_out, frame_bytes) ? rgba_out : nullptr;
+    const bool pageable = dst == nullptr;
+    if (pageable) {
+        if (!m->h_frame) {
+            (void)hipSetDevice(m->devs[0]);
+            if (!ok(hipHostMalloc(&m->h_frame, frame_bytes, hipHostMallocPortable))) {
+                (void)hipGetLastError();
+                m->h_frame = nullptr;
+                return RG_ERR_OUT_OF_MEMORY;
+            }
+        }
+        dst = static_cast<uint8_t *>(m->h_frame);
+    }
+    const uint32_t tiles = (H + T - 1) / T;
+    const uint32_t per_dev = (tiles + (uint32_t)n - 1) / (uint32_t)n;  // selected tiles of device 0 (the most)
+    const uint32_t J = (per_dev + (uint32_t)multi_bands(s, W, H, n) - 1) / (uint32_t)multi_bands(s, W, H, n);
+    const int K = (int)((per_dev + J - 1) / J);  // bands of J tiles per device (device 0's are all non-empty)
+    if (!ok(hipSetDevice(m->devs[0])) || !ok(hipEventRecord(m->ev0, m->streams[0]))) return RG_ERR_DEVICE;
+    for (int b = 0; b < K; ++b) {
+        for (int i = 0; i < n; ++i) {
+            const rg_tiling t = {T, (uint32_t)n, (uint32_t)i};
+            const uint32_t sel = (tiles > (uint32_t)i) ? (tiles - (uint32_t)i + (uint32_t)n - 1) / (uint32_t)n : 0u;
+            const uint32_t j0 = std::min(sel, (uint32_t)b * J), j1 = std::min(sel, j0 + J);
+            unsigned long long *snap = m->snap + 4 * ((size_t)i * K + b);
+            if (!ok(hipSetDevice(m->devs[i]))) return RG_ERR_DEVICE;
+            hipStream_t rs = (b & 1) ? m->streams2[i] : m->streams[i];
+            if (b == 1 && i == 0 && !ok(hipStreamWaitEvent(rs, m->ev0, 0))) return RG_ERR_DEVICE;
+            if (j1 == j0) {  // nothing of this device in this band
+                std::memset(snap, 0, 4 * sizeof(unsigned long long));
+                if (!ok(hipEventRecord(m->ev_copy[i][b], m->copies[i]))) return RG_ERR_DEVICE;
+                continue;
+            }
+            uint8_t *part = static_cast<uint8_t *>(m->parts[i]) + (size_t)j0 * T * row4;
+            rg_status st = rg_launch_tiles(m->reps[i], W, H, &t, part, nullptr, rs, snap, nullptr, false, nullptr,
+                                           0, nullptr, 3, false, false, j0, j1 - j0);
+            if (st != RG_OK) return st;
+            if (!ok(hipEventRecord(m->ev_band[i][b], rs)) || !ok(hipStreamWaitEvent(m->copies[i], m->ev_band[i][b], 0)))
+                return RG_ERR_DEVICE;
+            // selected tile j of device i is image tile j*n + i: whole tiles in one strided
+            // copy, the image's last (partial) tile, if it is this device's, on its own
+            const uint32_t last_j = (tiles - 1u - (uint32_t)i) / (uint32_t)n;  // valid: sel > 0
+            const bool has_partial = (tiles - 1u) % (uint32_t)n == (uint32_t)i && j1 - 1 == last_j && H % T != 0;
+            const uint32_t full = (j1 - j0) - (has_partial ? 1u : 0u);
+            uint8_t *d0 = dst + ((size_t)j0 * n + (size_t)i) * T * row4;
+            if (full > 0 && !ok(hipMemcpy2DAsync(d0, (size_t)n * T * row4, part, (size_t)T * row4, (size_t)T * row4,
+                                                 full, hipMemcpyDeviceToHost, m->copies[i])))
+                return RG_ERR_DEVICE;
+            if (has_partial) {
+                const uint32_t y0 = (tiles - 1u) * T;
+                if (!ok(hipMemcpyAsync(dst + (size_t)y0 * row4, part + (size_t)full * T * row4, (size_t)(H - y0) * row4,
+                                       hipMemcpyDeviceToHost, m->copies[i])))
+                    return RG_ERR_DEVICE;
+            }
+            if (!ok(hipEventRecord(m->ev_copy[i][b], m->copies[i]))) return RG_ERR_DEVICE;
+        }
+    }
+    // kernel_ms: device 0's renders (its last band on the second stream joined)
+    (void)hipSetDevice(m->devs[0]);
+    const int last_b = (K - 1) & 1 ? K - 1 : K - 2;  // last band on streams2 (odd index), -1: none
+    if (last_b > 0 && !ok(hipStreamWaitEvent(m->streams[0], m->ev_band[0][last_b], 0))) return RG_ERR_DEVICE;
+    if (!ok(hipEventRecord(m->ev1, m->streams[0]))) return RG_ERR_DEVICE;
+    if (pageable) {
+        // band b's image rows [b J n T, (b + 1) J n T) are complete once every device copied its part
+        rg_image_res &img = s->img;
+        if (!img.pool) img.pool = std::make_shared<rg_copy_pool>(RG_COPY_HELPERS);
+        struct Active {
+            rg_copy_pool &p;
+            explicit Active(rg_copy_pool &q) : p(q) { p.begin(); }
+            ~Active() { p.end(); }
+        } active(*img.pool);
+        for (int b = 0; b < K; ++b) {
+            for (int i = 0; i < n; ++i)
+                if (!ok(hipSetDevice(m->devs[i])) || !ok(hipEventSynchronize(m->ev_copy[i][b]))) return RG_ERR_DEVICE;
+            const size_t y0 = std::min<size_t>(H, (size_t)b * J * n * T), y1 = std::min<size_t>(H, (size_t)(b + 1) * J * n * T);
+            if (y1 > y0) img.pool->copy(rgba_out + y0 * row4, dst + y0 * row4, (y1 - y0) * row4);
+        }
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        if (!ok(hipSetDevice(m->devs[i]))) return RG_ERR_DEVICE;
+        for (hipStream_t x : {m->streams[i], m->streams2[i], m->copies[i]})
+            if (!ok(hipStreamSynchronize(x))) return RG_ERR_DEVICE;
+    }
+    return merge_snaps(m, K, stats);
 }
 
 }  // namespace
@@ -207,7 +477,8 @@ extern "C" rg_status rg_render_multi(const rg_scene *s, uint32_t W, uint32_t H, 
     if ((unsigned long long)H * W >= (1ull << 32)) return RG_ERR_INVALID_ARGUMENT;
     const uint32_t T = tile_rows ? tile_rows : 8u;
     rg_multi_res *m = s->multi;
-    if (!m || m->n != ngpus || m->w != W || m->h != H || m->T != T) {
+    if (!m || m->n != ngpus || m->w != W || m->h != H || m->T != T || m->mode != s->multi_mode ||
+        m->stand_in != s->multi_stand_in) {
         rg_multi_release(s);
         rg_status st = build_res(s, ngpus, W, H, T, &m);
         if (st != RG_OK) {
@@ -216,57 +487,16 @@ extern "C" rg_status rg_render_multi(const rg_scene *s, uint32_t W, uint32_t H, 
         }
         s->multi = m;
     }
-    const Rccl *r = rccl();
-    const int n = m->n;
-    for (int i = 1; i < n; ++i) rg_sync_settings(m->reps[i], s);
-    // renders
-    if (!ok(hipSetDevice(m->devs[0])) || !ok(hipEventRecord(m->ev0, m->streams[0]))) return RG_ERR_DEVICE;
-    for (int i = 0; i < n; ++i) {
-        const rg_tiling t = {T, (uint32_t)n, (uint32_t)i};
-        rg_status st = rg_launch_tiles(m->reps[i], W, H, &t, static_cast<uint8_t *>(m->parts[i]), nullptr,
-                                       m->streams[i], m->snap + 4 * i, nullptr);
-        if (st != RG_OK) return st;
-        if (i > 0 && !ok(rg_launch_pack_rgb(m->parts[i], m->packed[i], (size_t)m->slot_rows * W, m->streams[i])))
-            return RG_ERR_DEVICE;
-    }
-    // one gather of the equal-size parts to device 0 (all ranks' calls in one group)
-    if (r->group_start() != 0) return RG_ERR_COLLECTIVE;
-    int gerr = 0;
-    for (int i = 0; i < n; ++i) {
-        (void)hipSetDevice(m->devs[i]);
-        const int g = r->gather(i == 0 ? m->parts[i] : m->packed[i], i == 0 ? m->gathered : nullptr, m->slot_bytes,
-                                kNcclUint8, 0, m->comms[i],
-                                m->streams[i]);
-        if (g != 0 && g != kNcclInProgress && gerr == 0) gerr = g;
-    }
-    const int ge = r->group_end();
-    if (gerr != 0 || (ge != 0 && ge != kNcclInProgress)) return RG_ERR_COLLECTIVE;
-    // device 0: re-interleave, copy to the host
-    if (!ok(hipSetDevice(m->devs[0])) ||
-        !ok(rg_launch_reinterleave(m->gathered, m->parts[0], m->image, W, H, T, (uint32_t)n, m->slot_bytes,
-                                   m->streams[0])) ||
-        !ok(hipEventRecord(m->ev1, m->streams[0])) ||
-        !ok(hipMemcpyAsync(rgba_out, m->image, (size_t)H * W * 4, hipMemcpyDeviceToHost, m->streams[0])))
-        return RG_ERR_DEVICE;
-    for (int i = n - 1; i >= 0; --i)
-        if (!ok(hipSetDevice(m->devs[i])) || !ok(hipStreamSynchronize(m->streams[i]))) return RG_ERR_DEVICE;
-    rg_stats total;
-    std::memset(&total, 0, sizeof total);
-    total.error_pixel = -1;
-    unsigned long long worst = 0;  // complemented keys: the max is the lowest erroring pixel
-    for (int i = 0; i < n; ++i) {
-        total.rays.primary += m->snap[4 * i];
-        total.rays.shadow += m->snap[4 * i + 1];
-        total.rays.secondary += m->snap[4 * i + 2];
-        worst = std::max(worst, m->snap[4 * i + 3]);
-    }
-    unsigned long long w4[4] = {0, 0, 0, worst};
-    rg_stats es;
-    const rg_status err = rg_snap_status(w4, &es);
-    total.error_pixel = es.error_pixel;
-    float ms = 0.0f;
-    (void)hipEventElapsedTime(&ms, m->ev0, m->ev1);
-    total.kernel_ms = ms;
-    if (stats) *stats = total;
-    return err;
+    for (int i = 1; i < m->n; ++i) rg_sync_settings(m->reps[i], s);
+    const rg_status st = m->mode == 1 ? render_gather(s, m, rgba_out, stats) : render_direct(s, m, rgba_out, stats);
+    (void)hipSetDevice(s->device);
+    return st;
+}
+
+extern "C" rg_status rg_debug_set_multi(rg_scene *s, int32_t mode, int32_t stand_in, int32_t bands) {
+    if (!s || mode < 0 || mode > 1 || bands < 0 || bands > kMaxBands) return RG_ERR_INVALID_ARGUMENT;
+    s->multi_mode = mode;
+    s->multi_stand_in = stand_in != 0;
+    s->multi_bands = bands;
+    return RG_OK;
 }

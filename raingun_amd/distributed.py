@@ -292,7 +292,7 @@ class NativeFramePipeline:
     renders in ~55 us).  Uses the communicator of the torch.distributed "nccl"
     group and the RCCL library torch loaded."""
 
-    def __init__(self, scene_handle, width: int, height: int, rank: int, world: int, tile_rows: int = TILE_ROWS,
+    def __init__(self, scene, width: int, height: int, rank: int, world: int, tile_rows: int = TILE_ROWS,
                  depth: int = 4, group=None, device=None):
         import ctypes as C
 
@@ -300,6 +300,10 @@ class NativeFramePipeline:
 
         self.W, self.H, self.rank = width, height, rank
         self._lib = _abi.lib()
+        # a DeviceScene is kept alive as long as the pipeline (raingun_frames.h: the scene
+        # must outlive its frames); a raw handle is the caller's to keep
+        self._scene = scene
+        scene_handle = getattr(scene, "handle", scene)
         h = C.c_void_p()
         st = self._lib.rg_frames_create(scene_handle, width, height, tile_rows, rank, world, depth,
                                         C.c_void_p(rccl_comm_ptr(group, device)), C.c_void_p(rccl_gather_fn()),
@@ -331,6 +335,7 @@ class NativeFramePipeline:
         if getattr(self, "_h", None):
             self._lib.rg_frames_destroy(self._h)
             self._h = None
+        self._scene = None
 
     def __del__(self):
         try:
