@@ -493,12 +493,47 @@ def host_visible(workload: str, args, dev, W: int = 3840, H: int = 2160, budget_
                 reg.close()
         res[kind] = {"value": round(rays / dt / 1e6, 3), "ms_per_step": round(dt * 1e3, 4), "frames": n,
                      "frame_bytes": H * W * 4, "host_GBps": round(H * W * 4 / dt / 1e9, 2)}
+    res["multi_8gpu_rehearsal"] = multi_rehearsal(ds, W, H, res["pinned"]["ms_per_step"], args)
     ds.close()
     torch.cuda.synchronize(dev)
     res["value"] = res["pinned"]["value"]
     res["ms_per_step"] = res["pinned"]["ms_per_step"]
     res["unit"] = "Mrays/s"
     return res
+
+
+def multi_rehearsal(ds, W: int, H: int, one_gpu_ms: float, args, n: int = 8, budget_s: float = 0.5):
+    """rg_render_multi's host-visible frame on an n-GPU node, rehearsed on one GPU: each device's
+    timeline -- its row tiles rendered in bands, each band's rows copied over ITS OWN PCIe link
+    straight into the caller's page-locked buffer (rg_multi.hip, direct mode) -- timed alone
+    (rg_debug_set_multi stand-in, only_rank = r) for every r.  The frame is done when the slowest
+    device is: projected frame time = max over r.  A projection (this GPU's link stands for each
+    device's own; host memory bandwidth assumed to take n links at once), not a measurement."""
+    import numpy as np
+
+    from raingun_amd import _abi
+
+    buf = np.empty((H, W, 4), dtype=np.uint8)
+    reg = _abi.HostRegistration(buf)
+    per_rank = []
+    try:
+        for r in range(n):
+            ds.set_multi(0, stand_in=True, bands=0, only_rank=r)
+            for _ in range(2):
+                ds.render_multi(W, H, n, 8, out=buf)
+            k, t0 = 0, time.perf_counter()
+            while k < 5 or (time.perf_counter() - t0 < budget_s and k < args.steps):
+                ds.render_multi(W, H, n, 8, out=buf)
+                k += 1
+            per_rank.append((time.perf_counter() - t0) / k * 1e3)
+    finally:
+        ds.set_multi(0, stand_in=False, bands=0, only_rank=-1)
+        reg.close()
+    proj = max(per_rank)
+    return {"projected_ms_per_step": round(proj, 4), "projected_speedup_vs_1gpu": round(one_gpu_ms / proj, 2),
+            "per_device_ms": [round(x, 4) for x in per_rank], "n_gpus": n,
+            "basis": "one GPU times each device's rg_render_multi timeline alone (banded render of its 8-row tiles + "
+                     "its rows' strided copies into the pinned caller buffer); projected frame = the slowest device"}
 
 
 # Extra line items: (key, workload, size, CPU baseline?) -- BASELINE configs[2..4] and the north_star scene.

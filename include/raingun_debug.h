@@ -68,8 +68,17 @@ rg_status rg_debug_set_host_tile_shape(rg_scene *scene, int32_t tile_wlog);
  * re-interleave there, one copy to the host.  stand_in = 1 places every
  * "device" on the scene's device (a replica each) and routes mode 1's gather
  * through a stand-in with ncclGather's signature and group semantics, so
- * ngpus > 1 runs on one GPU (tests).  Results are identical for every setting. */
-rg_status rg_debug_set_multi(rg_scene *scene, int32_t mode, int32_t stand_in, int32_t bands);
+ * ngpus > 1 runs on one GPU (tests).  Results are identical for every setting.
+ * only_rank >= 0 (stand-in, mode 0 only) issues only that device's work -- its
+ * banded render and its rows' copies to the host -- so one GPU times the
+ * timeline one device of an N-GPU node runs (the frame is then incomplete);
+ * -1 = every device. */
+rg_status rg_debug_set_multi(rg_scene *scene, int32_t mode, int32_t stand_in, int32_t bands, int32_t only_rank);
+
+/* An rg_gather_fn (raingun_frames.h) that does nothing and returns 0: the
+ * frame loop's own host cost per frame without a collective (probes). */
+int rg_debug_gather_noop(const void *send, void *recv, size_t count, int datatype, int root, void *comm,
+                         void *stream);
 
 /* Copy the scene's 16 statistics words after the last render: [0..2] ray
  * counts, [4..8] BVH traversal statistics when the library was built with

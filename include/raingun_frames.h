@@ -42,6 +42,13 @@ rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t heigh
                            int32_t world, int32_t depth, void *comm, rg_gather_fn gather, rg_frames **out);
 void rg_frames_destroy(rg_frames *frames);
 
+/* Frames per gather: 2 (default when world > 1 and depth is even) gathers two
+ * consecutive frames' parts in ONE ncclGather, halving rank 0's per-frame
+ * enqueue cost; 1 gathers every frame on its own.  Call before the first
+ * rg_frames_step; batch must divide depth.  Frames and their order are the
+ * same either way (a batch cut short by rg_frames_flush is gathered then). */
+rg_status rg_frames_set_batch(rg_frames *frames, int32_t batch);
+
 /* Enqueue one frame (asynchronous: returns once its work is on the streams). */
 rg_status rg_frames_step(rg_frames *frames);
 

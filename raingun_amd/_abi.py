@@ -139,10 +139,10 @@ EXPORTED_SYMBOLS = (
 # include/raingun_debug.h
 DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
                  "rg_debug_set_tile_order", "rg_debug_set_lane_depth", "rg_debug_set_image_bands",
-                 "rg_debug_set_host_tile_shape", "rg_debug_set_multi")
+                 "rg_debug_set_host_tile_shape", "rg_debug_set_multi", "rg_debug_gather_noop")
 # include/raingun_frames.h
 FRAMES_SYMBOLS = ("rg_frames_create", "rg_frames_destroy", "rg_frames_step", "rg_frames_flush", "rg_frames_image",
-                  "rg_frames_read_image", "rg_frames_status")
+                  "rg_frames_read_image", "rg_frames_status", "rg_frames_set_batch")
 PATH_AUTO, PATH_LIGHT, PATH_HEAVY = -1, 0, 1
 
 
@@ -201,7 +201,7 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_set_image_bands.argtypes = [C.c_void_p, C.c_int32]
     if hasattr(lib, "rg_debug_set_multi"):  # absent from pre-round-3 builds
         lib.rg_debug_set_multi.restype = C.c_int32
-        lib.rg_debug_set_multi.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
+        lib.rg_debug_set_multi.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32]
     if hasattr(lib, "rg_debug_set_host_tile_shape"):  # absent from older builds A/B runs load (RAINGUN_HIP_LIB)
         lib.rg_debug_set_host_tile_shape.restype = C.c_int32
         lib.rg_debug_set_host_tile_shape.argtypes = [C.c_void_p, C.c_int32]
@@ -235,6 +235,9 @@ def _declare(lib: C.CDLL) -> None:
                                     P(rg_stats)]
     lib.rg_frames_status.restype = C.c_int32
     lib.rg_frames_status.argtypes = [C.c_void_p, P(C.c_int32)]
+    if hasattr(lib, "rg_frames_set_batch"):  # absent from pre-round-3 builds
+        lib.rg_frames_set_batch.restype = C.c_int32
+        lib.rg_frames_set_batch.argtypes = [C.c_void_p, C.c_int32]
 
 
 def lib() -> C.CDLL:

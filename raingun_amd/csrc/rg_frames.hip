@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/raingun.h"
+#include "../../include/raingun_debug.h"
 #include "../../include/raingun_frames.h"
 #include "rg_internal.h"
 
@@ -121,10 +122,12 @@ struct rg_frames {
     rg_gather_fn gather = nullptr;
     std::vector<hipStream_t> render;
     hipStream_t comm_stream = nullptr, side = nullptr;
-    std::vector<void *> parts, packed, gathered, image;
+    std::vector<void *> parts, packed, gathered, image;  // parts/image per slot; packed/gathered per batch
     std::vector<hipEvent_t> rendered, sent, done;
     unsigned long long k = 0;
     int last = -1;
+    int batch = 1;              // frames per gather (consecutive slots of one batch)
+    int pend_b0 = 0, pend_n = 0;  // rendered frames of the current batch not gathered yet
     rg_status err = RG_OK;     // first device error of any frame (sticky until destroy)
     int32_t err_pixel = -1;
 };
@@ -208,18 +211,23 @@ rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t heigh
         good = good && ok(hipMalloc(&p, bytes)) && ok(hipMemset(p, 0, bytes));  // padding rows stay zero
         v.push_back(p);
     };
+    // two frames per gather halve rank 0's per-frame enqueue cost (RCCL's host work
+    // is per call); a depth that is not even keeps one
+    f->batch = (world > 1 && depth % 2 == 0) ? 2 : 1;
+    const int B = 2;  // buffers sized for the largest batch (rg_frames_set_batch)
     f->render.assign(depth, nullptr);
     for (int b = 0; b < depth && good; ++b) {
         stream(f->render[b]);
-        alloc(f->parts, std::max(f->part_bytes, f->slot_bytes));  // the root sends its part's first slot_bytes
+        // the root sends (and ignores) the first batch * slot_bytes of its RGBA part
+        alloc(f->parts, std::max(f->part_bytes, f->slot_bytes * B));
         event(f->rendered);
         event(f->sent);
         event(f->done);
         if (rank == 0) {
-            alloc(f->gathered, f->slot_bytes * (size_t)world);
+            alloc(f->gathered, f->slot_bytes * B * (size_t)world);
             alloc(f->image, (size_t)height * width * 4);
         } else {
-            alloc(f->packed, f->slot_bytes);
+            alloc(f->packed, f->slot_bytes * B);
         }
     }
     stream(f->comm_stream);
@@ -235,6 +243,56 @@ rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t heigh
 
 void rg_frames_destroy(rg_frames *f) { frames_release(f); }
 
+}  // extern "C"
+
+namespace {
+
+// ONE gather for the n consecutive frames of slots b0 .. b0 + n - 1 (one batch):
+// rank r's chunk of the receive buffer holds its n packed parts back to back.
+rg_status issue_gather(rg_frames *f, int b0, int n) {
+    const int B = 2;
+    const int p = b0 / B, h0 = b0 % B;  // the batch's buffers, the first frame's place in them
+    const size_t count = (size_t)n * f->slot_bytes;
+    void *send = f->rank == 0 ? f->parts[b0] : static_cast<uint8_t *>(f->packed[p]) + (size_t)h0 * f->slot_bytes;
+    // a batch cut short by a flush leaves the batch's later frames their own part of the
+    // buffers (send: slot h; receive: from h0 * world slots on), so the next frames'
+    // gather never overwrites what the root's re-interleave of this one still reads
+    void *recv = f->rank == 0 ? static_cast<uint8_t *>(f->gathered[p]) + (size_t)h0 * f->world * f->slot_bytes : nullptr;
+    // ncclUint8 = 1 (rccl.h); recvbuff may be NULL off the root.  ncclSuccess = 0;
+    // a non-blocking communicator may answer ncclInProgress = 7 with the operation enqueued
+    const int gr = f->gather(send, recv, count, 1, 0, f->comm, f->comm_stream);
+    if (gr != 0 && gr != 7) return RG_ERR_DEVICE;
+    if (!ok(hipEventRecord(f->sent[b0], f->comm_stream))) return RG_ERR_DEVICE;
+    if (f->rank == 0 && !ok(hipStreamWaitEvent(f->side, f->sent[b0], 0))) return RG_ERR_DEVICE;
+    for (int h = 0; h < n; ++h) {
+        const int b = b0 + h;
+        if (f->rank == 0) {
+            if (!ok(rg_launch_reinterleave(static_cast<uint8_t *>(recv) + (size_t)h * f->slot_bytes, f->parts[b],
+                                           f->image[b], f->w, f->h, f->T, (uint32_t)f->world, count, f->side)) ||
+                !ok(hipEventRecord(f->done[b], f->side)))
+                return RG_ERR_DEVICE;
+        } else if (!ok(hipEventRecord(f->done[b], f->comm_stream))) {
+            return RG_ERR_DEVICE;
+        }
+    }
+    f->last = b0 + n - 1;
+    f->pend_n = 0;
+    return RG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// raingun_debug.h: a gather that does nothing (host-overhead probes of the frame loop)
+int rg_debug_gather_noop(const void *, void *, size_t, int, int, void *, void *) { return 0; }
+
+rg_status rg_frames_set_batch(rg_frames *f, int32_t batch) {
+    if (!f || batch < 1 || batch > 2 || f->depth % batch != 0 || f->k != 0) return RG_ERR_INVALID_ARGUMENT;
+    f->batch = batch;
+    return RG_OK;
+}
+
 rg_status rg_frames_step(rg_frames *f) {
     if (!f || !f->scene) return RG_ERR_INVALID_ARGUMENT;
     const int b = (int)(f->k % (unsigned long long)f->depth);
@@ -243,33 +301,28 @@ rg_status rg_frames_step(rg_frames *f) {
     rg_status st = rg_render_tiles_pipelined(f->scene, f->w, f->h, &f->tiling, static_cast<uint8_t *>(f->parts[b]),
                                              nullptr, rs);
     if (st != RG_OK) return st;
-    // off the root the part travels packed (3 B per pixel); the root's own part is read in place
-    if (f->rank != 0 && !ok(rg_launch_pack_rgb(f->parts[b], f->packed[b], (size_t)f->slot_rows * f->w, rs)))
+    // off the root the part travels packed (3 B per pixel) in its batch's send buffer;
+    // the root's own part is read in place
+    const int B = 2, p = b / B, h = b % B;
+    if (f->rank != 0 && !ok(rg_launch_pack_rgb(f->parts[b], static_cast<uint8_t *>(f->packed[p]) + (size_t)h * f->slot_bytes,
+                                               (size_t)f->slot_rows * f->w, rs)))
         return RG_ERR_DEVICE;
     if (!ok(hipEventRecord(f->rendered[b], rs)) || !ok(hipStreamWaitEvent(f->comm_stream, f->rendered[b], 0)))
         return RG_ERR_DEVICE;
-    // ncclUint8 = 1 (rccl.h); recvbuff may be NULL off the root.  ncclSuccess = 0;
-    // a non-blocking communicator may answer ncclInProgress = 7 with the operation enqueued
-    const int gr = f->gather(f->rank == 0 ? f->parts[b] : f->packed[b], f->rank == 0 ? f->gathered[b] : nullptr,
-                             f->slot_bytes, 1, 0, f->comm, f->comm_stream);
-    if (gr != 0 && gr != 7) return RG_ERR_DEVICE;
-    if (!ok(hipEventRecord(f->sent[b], f->comm_stream))) return RG_ERR_DEVICE;
-    if (f->rank == 0) {
-        if (!ok(hipStreamWaitEvent(f->side, f->sent[b], 0))) return RG_ERR_DEVICE;
-        if (!ok(rg_launch_reinterleave(f->gathered[b], f->parts[b], f->image[b], f->w, f->h, f->T,
-                                       (uint32_t)f->world, f->slot_bytes, f->side)) ||
-            !ok(hipEventRecord(f->done[b], f->side)))
-            return RG_ERR_DEVICE;
-    } else if (!ok(hipEventRecord(f->done[b], f->comm_stream))) {
-        return RG_ERR_DEVICE;
-    }
-    f->last = b;
+    if (f->pend_n == 0) f->pend_b0 = b;
+    f->pend_n++;
     f->k++;
+    // a batch is gathered when its last slot is rendered (every rank issues the same gathers)
+    if ((b + 1) % f->batch == 0) return issue_gather(f, f->pend_b0, f->pend_n);
     return RG_OK;
 }
 
 rg_status rg_frames_flush(rg_frames *f) {
     if (!f || !f->scene) return RG_ERR_INVALID_ARGUMENT;
+    if (f->pend_n > 0) {  // a batch cut short: gather what was rendered (every rank flushes at the same frame)
+        const rg_status st = issue_gather(f, f->pend_b0, f->pend_n);
+        if (st != RG_OK) return st;
+    }
     for (hipStream_t s : f->render) {
         if (!ok(hipStreamSynchronize(s))) return RG_ERR_DEVICE;
         // device errors of this rank's renders (the reference panics: rendering.rs, bodies.rs:324, scene.rs:38)
@@ -298,9 +351,10 @@ const uint8_t *rg_frames_image(const rg_frames *f) {
 }
 
 rg_status rg_frames_read_image(const rg_frames *f, uint8_t *host_out) {
-    if (!f || !host_out || f->rank != 0 || f->last < 0) return RG_ERR_INVALID_ARGUMENT;
-    const rg_status st = rg_frames_flush(const_cast<rg_frames *>(f));
-    if (st == RG_ERR_DEVICE) return st;
+    if (!f || !host_out || f->rank != 0) return RG_ERR_INVALID_ARGUMENT;
+    const rg_status st = rg_frames_flush(const_cast<rg_frames *>(f));  // gathers a batch cut short
+    if (st == RG_ERR_DEVICE || st == RG_ERR_INVALID_ARGUMENT) return st;
+    if (f->last < 0) return RG_ERR_INVALID_ARGUMENT;  // no frame yet
     if (!ok(hipMemcpy(host_out, f->image[f->last], (size_t)f->h * f->w * 4, hipMemcpyDeviceToHost)))
         return RG_ERR_DEVICE;
     return st;  // the frame is delivered; a device error any frame raised is reported

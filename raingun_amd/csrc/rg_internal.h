@@ -168,6 +168,7 @@ struct rg_scene {
     int multi_mode = 0;
     bool multi_stand_in = false;
     int multi_bands = 0;
+    int multi_only_rank = -1;  // stand-in direct mode: issue only this device's work (timeline rehearsal)
     std::shared_ptr<const rg_host_tables> host;
     mutable std::vector<rg_launch_ctx *> ctxs;  // one per stream used
     mutable rg_launch_ctx *last = nullptr;       // the context of the latest launch (rg_debug_counters)

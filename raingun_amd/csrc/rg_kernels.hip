@@ -2513,7 +2513,9 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
     // scenes: the body loop dominates and waves mix ray kinds -> one ray per
     // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
     const bool heavy = rg_heavy_path(*a);
+#ifndef RG_DEV_HEAVY_ONLY  // development builds: resource reports of the heavy kernels only
     if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream, gt);
+#endif
 #ifdef RG_DEV_LIGHT_ONLY  // development builds: resource reports of the light kernels only
     return hipErrorNotSupported;
 #else

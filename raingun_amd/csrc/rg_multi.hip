@@ -398,7 +398,8 @@ rg_status render_direct(const rg_scene *s, rg_multi_res *m, uint8_t *rgba_out, r
         for (int i = 0; i < n; ++i) {
             const rg_tiling t = {T, (uint32_t)n, (uint32_t)i};
             const uint32_t sel = (tiles > (uint32_t)i) ? (tiles - (uint32_t)i + (uint32_t)n - 1) / (uint32_t)n : 0u;
-            const uint32_t j0 = std::min(sel, (uint32_t)b * J), j1 = std::min(sel, j0 + J);
+            uint32_t j0 = std::min(sel, (uint32_t)b * J), j1 = std::min(sel, j0 + J);
+            if (s->multi_only_rank >= 0 && i != s->multi_only_rank) j1 = j0;  // timeline rehearsal of one device
             unsigned long long *snap = m->snap + 4 * ((size_t)i * K + b);
             if (!ok(hipSetDevice(m->devs[i]))) return RG_ERR_DEVICE;
             hipStream_t rs = (b & 1) ? m->streams2[i] : m->streams[i];
@@ -493,10 +494,13 @@ extern "C" rg_status rg_render_multi(const rg_scene *s, uint32_t W, uint32_t H, 
     return st;
 }
 
-extern "C" rg_status rg_debug_set_multi(rg_scene *s, int32_t mode, int32_t stand_in, int32_t bands) {
-    if (!s || mode < 0 || mode > 1 || bands < 0 || bands > kMaxBands) return RG_ERR_INVALID_ARGUMENT;
+extern "C" rg_status rg_debug_set_multi(rg_scene *s, int32_t mode, int32_t stand_in, int32_t bands,
+                                        int32_t only_rank) {
+    if (!s || mode < 0 || mode > 1 || bands < 0 || bands > kMaxBands || only_rank < -1) return RG_ERR_INVALID_ARGUMENT;
+    if (only_rank >= 0 && (mode != 0 || !stand_in)) return RG_ERR_INVALID_ARGUMENT;
     s->multi_mode = mode;
     s->multi_stand_in = stand_in != 0;
     s->multi_bands = bands;
+    s->multi_only_rank = only_rank;
     return RG_OK;
 }

@@ -282,10 +282,11 @@ class DeviceScene:
         """Row bands of host-visible renders (0: by frame size; include/raingun_debug.h)."""
         _abi.check(_abi.lib().rg_debug_set_image_bands(self.handle, int(bands)))
 
-    def set_multi(self, mode: int = 0, stand_in: bool = False, bands: int = 0) -> None:
+    def set_multi(self, mode: int = 0, stand_in: bool = False, bands: int = 0, only_rank: int = -1) -> None:
         """rg_render_multi delivery (raingun_debug.h): 0 per-device copies to the host, 1 RCCL gather;
-        stand_in: every device is this one (ngpus > 1 on one GPU)."""
-        _abi.check(_abi.lib().rg_debug_set_multi(self.handle, int(mode), 1 if stand_in else 0, int(bands)))
+        stand_in: every device is this one (ngpus > 1 on one GPU); only_rank: rehearse one device's work."""
+        _abi.check(_abi.lib().rg_debug_set_multi(self.handle, int(mode), 1 if stand_in else 0, int(bands),
+                                                 int(only_rank)))
 
     def set_host_tile_shape(self, tile_wlog: int) -> None:
         """Tile shape of one-launch host-visible renders: log2 of the tile width, 3 (8x8) .. 6 (64x1)."""

@@ -53,10 +53,10 @@ sh = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 def launch(part=None, s=None):
     p = buf if part is None else part
     st = sh if s is None else C.c_void_p(s.cuda_stream)
-    _abi.check(lib.rg_render_tiles_async(ds.handle, W, H, C.byref(tiling), C.c_void_p(p.data_ptr()), None, st, None))
+    _abi.check(lib.rg_render_tiles_pipelined(ds.handle, W, H, C.byref(tiling), C.c_void_p(p.data_ptr()), None, st))
 
 
-timed("rg_render_tiles_async", launch)
+timed("rg_render_tiles_pipelined", launch)
 for f, gather in ((1, False), (4, False), (4, True)):
     pipe = rd.FramePipeline((slot, W, 4), H, 0, 1, T, device=dev, depth=f, streams=f > 1, gather=gather)
     timed(f"pipeline_F{f}{'_gather' if gather else ''}",
@@ -74,6 +74,24 @@ _abi.check(lib.rg_frames_create(ds.handle, W, H, T, 0, 1, 4, C.c_void_p(1), C.ca
 timed("native_pipeline_F4_noop_gather", lambda: _abi.check(lib.rg_frames_step(h)))
 lib.rg_frames_flush(h)
 lib.rg_frames_destroy(h)
+# rank 0 of an 8-rank loop: the library's native no-op gather in place of
+# ncclGather, so the numbers are the loop's own host work per frame; two frames per gather
+# (batch 2, the default at world > 1) halve the per-frame gather and bookkeeping calls
+noop = C.cast(lib.rg_debug_gather_noop, C.c_void_p)
+for world in (8,):
+    for batch in (1, 2):
+        h = C.c_void_p()
+        _abi.check(lib.rg_frames_create(ds.handle, W, H, T, 0, world, 8, C.c_void_p(1), noop, C.byref(h)))
+        _abi.check(lib.rg_frames_set_batch(h, batch))
+        timed(f"native_pipeline_world{world}_rank0_F8_batch{batch}_noop_gather",
+              lambda: _abi.check(lib.rg_frames_step(h)))
+        _abi.check(lib.rg_frames_flush(h))
+        lib.rg_frames_destroy(h)
+# RCCL's own host cost per ncclGather call (world 1): what batching halves per frame
+native = rd.NativeFramePipeline(ds.handle, W, H, 0, 1, T, depth=8, device=dev)
+timed("native_pipeline_F8_world1_rccl_gather", native.step)
+native.flush()
+native.close()
 recv = [torch.empty_like(buf)]
 timed("dist.gather_alone", lambda: dist.gather(buf, recv, dst=0, async_op=True))
 print(json.dumps(out, indent=1))

@@ -72,22 +72,27 @@ def _fake_gather(world, others, calls):
     on the stream the pipeline hands over, as RCCL would."""
     hip = _hip_runtime()
 
+    slot = others[1].numel() if world > 1 else 0
+
     def gather(send, recv, count, dtype, root, comm, stream):
         assert dtype == 1 and root == 0 and recv
         calls.append(count)
         if hip.hipMemcpyAsync(recv, send, count, 3, stream) != 0:  # hipMemcpyDeviceToDevice
             return 1
+        # a batch of count // slot frames: rank r's chunk holds its packed parts back to back
         for r in range(1, world):
-            if hip.hipMemcpyAsync(recv + r * count, others[r].data_ptr(), count, 3, stream) != 0:
-                return 1
+            for h in range(count // slot):
+                if hip.hipMemcpyAsync(recv + r * count + h * slot, others[r].data_ptr(), slot, 3, stream) != 0:
+                    return 1
         return 0
 
     return GATHER_FN(gather)
 
 
-@pytest.mark.parametrize("world,w,h,T,depth", [(2, 320, 243, 8, 3), (3, 256, 144, 16, 2), (8, 640, 357, 8, 4),
-                                               (8, 97, 61, 8, 1)])
-def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, depth):
+@pytest.mark.parametrize("world,w,h,T,depth,batch", [(2, 320, 243, 8, 3, 1), (3, 256, 144, 16, 2, 2),
+                                                     (8, 640, 357, 8, 4, 2), (8, 640, 357, 8, 4, 1),
+                                                     (8, 97, 61, 8, 1, 1), (2, 64, 40, 8, 8, 0)])
+def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, depth, batch):
     """The N > 1 native loop on one GPU: rank 0 of `world` ranks,
     the other ranks' parts (tiling {T, world, r}) pre-rendered and delivered by
     a stand-in gather.  The re-interleave, the slot offsets and the padding of
@@ -116,16 +121,24 @@ def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, de
     hdl = C.c_void_p()
     _abi.check(lib.rg_frames_create(ds.handle, w, h, T, 0, world, depth, C.c_void_p(1), C.cast(fn, C.c_void_p),
                                     C.byref(hdl)))
+    if batch:  # 0: the default (two frames per gather at world > 1 with an even depth)
+        _abi.check(lib.rg_frames_set_batch(hdl, batch))
     out = np.empty((h, w, 4), np.uint8)
     for k in range(2 * depth + 1):
         _abi.check(lib.rg_frames_step(hdl))
-        if k % 2 == 0:
+        if k % 3 == 0:  # read_image flushes: batches cut short are gathered then
             _abi.check(lib.rg_frames_read_image(hdl, out.ctypes.data))
             assert np.array_equal(out, ref), k
     _abi.check(lib.rg_frames_flush(hdl))
+    _abi.check(lib.rg_frames_read_image(hdl, out.ctypes.data))
+    assert np.array_equal(out, ref)
     lib.rg_frames_destroy(hdl)
     ds.close()
-    assert calls and all(c == slot_bytes for c in calls)
+    b = batch or (2 if depth % 2 == 0 else 1)
+    assert calls and all(c in (slot_bytes, b * slot_bytes) for c in calls)
+    assert sum(calls) == (2 * depth + 1) * slot_bytes  # every frame gathered exactly once
+    if b == 2:
+        assert 2 * slot_bytes in calls
 
 
 def test_native_pipeline_reports_device_errors():
