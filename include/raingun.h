@@ -172,7 +172,11 @@ rg_status rg_scene_set_max_depth(rg_scene *scene, uint32_t max_recursion_depth);
  * bands whose device-to-host copies overlap the later bands' renders (the DMA
  * lands directly in a pinned buffer; a pageable one is filled from pinned
  * staging by several host threads).  Any max_recursion_depth renders (scene.rs:16 is a u32): depths
- * above 65 keep their shading frames in device memory.  On a device error
+ * above 65 keep their shading frames in device memory, 88 B per open frame
+ * per thread of a persistent grid; when that exceeds half the free device
+ * memory (capped at 16 GiB) the grid shrinks to fit -- slower, same frame --
+ * and only when a single block's frames do not fit does the call return
+ * RG_ERR_OUT_OF_MEMORY (depth ~ 10^6 and up).  On a device error
  * (RG_ERR_AABB_NORMAL / _NAN_DISTANCE / _TRANSMISSION: the reference's
  * panics) the frame is still delivered and stats->error_pixel names the first
  * (lowest-index) pixel that raised it. */

@@ -511,10 +511,16 @@ int32_t rgo_render(const rg_scene_desc *s, uint32_t w, uint32_t h, const rg_tili
     pthread_mutex_init(&j.mu, NULL);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
+    /* every worker on a thread of its own with a large stack: the restatement
+     * recurses like the reference (rendering.rs:122-130), one call chain per
+     * ray depth, and recursion depths of 10^4 and more need ~0.5 KB per level */
     pthread_t th[256];
-    for (int i = 1; i < nthreads; ++i) pthread_create(&th[i], NULL, worker, &j);
-    worker(&j);
-    for (int i = 1; i < nthreads; ++i) pthread_join(th[i], NULL);
+    pthread_attr_t attr;
+    pthread_attr_init(&attr);
+    pthread_attr_setstacksize(&attr, (size_t)512 << 20);
+    for (int i = 0; i < nthreads; ++i) pthread_create(&th[i], &attr, worker, &j);
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+    pthread_attr_destroy(&attr);
     pthread_mutex_destroy(&j.mu);
     if (counts) *counts = j.counts;
     if (error_pixel) *error_pixel = j.err_pixel;

@@ -308,7 +308,20 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
         size_t threads = 0;
         if (!ok(rg_render_grid_threads(&a, disp, &threads)) || threads == 0 || threads > 0xFFFFFFFFull)
             return RG_ERR_DEVICE;
-        const size_t bytes = threads * (size_t)frames * RG_FRAME_BYTES;
+        const size_t per_thread = (size_t)frames * RG_FRAME_BYTES;
+        if (threads * per_thread > ((size_t)1 << 30)) {
+            // very deep recursion (scene.rs:16 is a u32): a persistent grid that fits half the free
+            // device memory (at most 16 GiB of frames) -- fewer waves, every depth still renders
+            size_t free_b = 0, total_b = 0;
+            if (!ok(hipMemGetInfo(&free_b, &total_b))) return RG_ERR_DEVICE;
+            const size_t budget = std::min<size_t>(free_b / 2, (size_t)16 << 30);
+            if (threads * per_thread > budget) {
+                a.max_grid_threads = (uint32_t)std::min<size_t>(budget / per_thread, 0xFFFFFFFFu);
+                if (!ok(rg_render_grid_threads(&a, disp, &threads)) || threads == 0) return RG_ERR_DEVICE;
+                if (threads * per_thread > budget) return RG_ERR_OUT_OF_MEMORY;  // not even one block fits
+            }
+        }
+        const size_t bytes = threads * per_thread;
         if (bytes > cx->deep_bytes) {
             if (cx->deep) (void)hipFree(cx->deep);
             cx->deep = nullptr;
@@ -377,12 +390,18 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
         }
     }
     cx->last_counters = a.counters;
+    // statistics words: written into page-locked host memory by the kernel's last wave, or copied
+    unsigned long long *snap_dev = (snap && out_rows > 0)
+                                       ? static_cast<unsigned long long *>(rg_host_device_ptr(snap, 4 * sizeof(*snap)))
+                                       : nullptr;
+    a.snap_out = snap_dev;
     if (out_rows > 0) {
         if (!ok(rg_launch_render(&a, disp, st))) return RG_ERR_DEVICE;
         cx->cur = 1 - cx->cur;  // the kernel zeroes the other set for the next launch
     }
     if (timed && !ok(hipEventRecord(cx->ev1, st))) return RG_ERR_DEVICE;
-    if (snap && !ok(hipMemcpyAsync(snap, a.counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st)))
+    if (snap && !snap_dev &&
+        !ok(hipMemcpyAsync(snap, a.counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st)))
         return RG_ERR_DEVICE;
     return RG_OK;
 }

@@ -173,6 +173,10 @@ struct RgKernelArgs {
     // (double)width, (double)height (ray.rs:46-51 divisions): kernel arguments land in SGPRs,
     // where the kernel's own conversions would hold two loop-invariant VGPR pairs
     double width_d, height_d;
+    // nullable, host memory the device can write: the last wave of the launch to finish copies
+    // the 4 statistics words (rays by class, error key) there -- no copy after the kernel
+    unsigned long long *snap_out;
+    uint32_t max_grid_threads;  // nonzero: cap on the persistent grid (the deep frame buffer's memory bound)
 };
 
 __host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }
@@ -211,7 +215,8 @@ __host__ __device__ __forceinline__ bool rg_heavy_path(const RgKernelArgs &a) {
     return heavy;
 }
 
-#define RG_COUNTER_WORDS (16 + 16 * 16)  // stats + 16 queue heads, 128 B apart
+#define RG_COUNTER_WORDS (16 + 16 * 16 + 16)  // stats + 16 queue heads, 128 B apart + the finished-wave count
+#define RG_DONE_WORD (16 + 16 * 16)            // waves of the launch that finished (RgKernelArgs::snap_out)
 
 // counters[3] holds ~((pixel << 8) | -status) of the lowest erroring pixel
 // (atomicMax of the complement); 0 = no error, so one memset resets all four.

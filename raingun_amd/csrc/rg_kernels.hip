@@ -18,6 +18,7 @@
 // Division and sqrt are the correctly-rounded hipcc expansions.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <mutex>
 #include <type_traits>
 #include <utility>
@@ -2208,6 +2209,18 @@ void rg_render_kernel(RgKernelArgs a) {
         if (p64) atomicAdd(&a.counters[0], p64);
         if (s64) atomicAdd(&a.counters[1], s64);
         if (q64) atomicAdd(&a.counters[2], q64);
+        if (a.snap_out) {
+            // the last wave to finish hands the statistics words to the host itself (the copy
+            // after the kernel would be a blit kernel of its own on the stream): this wave's
+            // counter atomics are complete before it is counted
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long waves = (unsigned long long)gridDim.x * (blockDim.x >> 6);
+            if (atomicAdd(&a.counters[RG_DONE_WORD], 1ull) == waves - 1ull) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    a.snap_out[k] = __hip_atomic_load(&a.counters[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
 }
 
@@ -2470,6 +2483,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     constexpr unsigned long long kmax = MAXD == 0 ? 0 : LB > 1 ? RG_LIGHT_TILES_PER_WAVE : RG_HEAVY_TILES_PER_WAVE;
     if constexpr (kmax > 0)  // non-persistent: one wave per kmax tiles
         blocks = (tiles + waves * kmax - 1) / (waves * kmax);
+    if (a->max_grid_threads && blocks * threads > a->max_grid_threads) blocks = a->max_grid_threads / threads;
     if (blocks < 1) blocks = 1;
     if (grid_threads) {
         *grid_threads = (size_t)blocks * threads;

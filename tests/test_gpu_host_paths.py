@@ -369,6 +369,25 @@ def test_recursion_deeper_than_compiled_frames(oracle_lib, path, depth):
     assert float(np.abs(rgb - o_rgb).max()) <= RGB_TOL
 
 
+@pytest.mark.parametrize("path", PATHS)
+def test_recursion_depth_20000_grid_capped(oracle_lib, path):
+    """at depth 20000 a full persistent grid's frames (88 B x 19999 per
+    thread) would need 230-350 GB; the launch caps the grid at half the free device
+    memory (<= 16 GiB of frames) and the frame renders, equal to the restatement."""
+    scene = _mirror_corridor(20000)
+    w, h = 16, 9
+    o_st, o_rgba, o_rgb, o_counts, _ = _oracle(oracle_lib, scene, w, h)
+    assert o_st == 0
+    assert o_counts["secondary"] > w * h * 5000
+    ds = DeviceScene(scene, path=path)
+    st = _abi.rg_stats()
+    rgba, rgb = ds.render_tiles(w, h, want_rgb=True, stats=st)
+    ds.close()
+    assert st.rays.as_dict() == o_counts
+    assert np.array_equal(rgba, o_rgba)
+    assert float(np.abs(rgb - o_rgb).max()) <= RGB_TOL
+
+
 # ---------------------------------------------------------------- rg_render_multi
 @pytest.mark.parametrize("kind,w,h,tile_rows", [("test1", 320, 243, 8), ("synth200", 256, 144, 16),
                                                 ("test3", 97, 61, 0)])
