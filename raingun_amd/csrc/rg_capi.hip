@@ -136,6 +136,8 @@ void release(rg_scene *s) {
     release_image_res(s->img);
     for (void *p : s->allocations) (void)hipFree(p);
     s->allocations.clear();
+    if (s->lds_blob) (void)hipFree(s->lds_blob);
+    s->lds_blob = nullptr;
     for (rg_launch_ctx *c : s->ctxs) destroy_ctx(c);
     s->ctxs.clear();
     delete s;
@@ -177,6 +179,8 @@ bool tiling_valid(const rg_tiling *t) {
 }
 
 int frames_needed(uint32_t max_depth) { return max_depth > 1 ? (int)max_depth - 1 : 1; }
+
+const void *lds_blob_for(const rg_scene *s, const RgKernelArgs &a);  // below
 
 // decode the complemented error key of counters[3] / a sticky word
 rg_status decode_error(unsigned long long word, int32_t *pixel) {
@@ -361,6 +365,7 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     }
     a.prim_sx = cx->prim;
     a.prim_sy = cx->prim + width;
+    if (!rg_heavy_path(a)) a.lds_blob = lds_blob_for(s, a);  // light path: one staging loop per block
     if (timed && !ok(hipEventRecord(cx->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
     if (s->tile_order == 1 || (s->tile_order < 0 && rg_heavy_path(a))) {
         const size_t ntiles = (size_t)rg_tile_count(a);
@@ -482,7 +487,46 @@ rg_status upload_tables(rg_scene *s, const rg_host_tables &h) {
         texs[i].texels = dp;
     }
     if (st == RG_OK) st = upload(s, &s->texs, texs.data(), texs.size());
+    s->tex_desc = texs;
     return st;
+}
+
+// The LDS arena of launch args `a` as one device image (light path: RgKernelArgs::lds_blob),
+// built from the host tables once per arena layout; nullptr if it cannot be made.
+const void *lds_blob_for(const rg_scene *s, const RgKernelArgs &a) {
+    const uint32_t layout[14] = {a.lds_sphf, a.lds_sph, a.lds_cc, a.lds_nodes, a.lds_pln, a.lds_dsk, a.lds_box,
+                                 a.lds_bodies, a.lds_mats, a.lds_lights, a.lds_texs, a.lds_total_bytes,
+                                 (uint32_t)a.n_nodes, (uint32_t)a.n_sph};
+    rg_scene *m = const_cast<rg_scene *>(s);
+    if (m->lds_blob && std::memcmp(layout, m->lds_blob_layout, sizeof layout) == 0) return m->lds_blob;
+    if (!s->host || a.lds_total_bytes == 0 || a.lds_total_bytes % 16u != 0u) return nullptr;
+    const rg_host_tables &h = *s->host;
+    std::vector<unsigned char> img(a.lds_total_bytes, 0);
+    auto put = [&](uint32_t off, const void *src, size_t bytes) {
+        if (bytes && off + bytes <= img.size()) std::memcpy(img.data() + off, src, bytes);
+    };
+    put(a.lds_sphf, h.sphf.data(), h.sphf.size() * sizeof(RgSphF));
+    put(a.lds_sphf + (uint32_t)(h.sphf.size() * sizeof(RgSphF)), h.sphf2.data(), h.sphf2.size() * sizeof(RgSphF2));
+    put(a.lds_sph, h.sph.data(), h.sph.size() * sizeof(RgSph));
+    put(a.lds_cc, h.sph_cc.data(), h.sph_cc.size() * sizeof(double));
+    if (a.n_nodes > 0) put(a.lds_nodes, h.nodes.data(), h.nodes.size() * sizeof(RgBvhNode));
+    put(a.lds_pln, h.pln.data(), h.pln.size() * sizeof(RgPln));
+    put(a.lds_dsk, h.dsk.data(), h.dsk.size() * sizeof(RgDsk));
+    put(a.lds_box, h.box.data(), h.box.size() * sizeof(RgBox));
+    put(a.lds_bodies, h.bodies.data(), h.bodies.size() * sizeof(RgBodyDev));
+    put(a.lds_mats, h.mats.data(), h.mats.size() * sizeof(RgMatDev));
+    put(a.lds_lights, h.lights.data(), h.lights.size() * sizeof(RgLightDev));
+    put(a.lds_texs, s->tex_desc.data(), s->tex_desc.size() * sizeof(RgTexDev));
+    void *p = nullptr;
+    if (!ok(hipMalloc(&p, img.size()))) { (void)hipGetLastError(); return nullptr; }
+    if (!ok(hipMemcpy(p, img.data(), img.size(), hipMemcpyHostToDevice))) { (void)hipFree(p); return nullptr; }
+    if (m->lds_blob) {
+        // stream-ordered launches may still read the old image: keep it with the scene's allocations
+        m->allocations.push_back(m->lds_blob);
+    }
+    m->lds_blob = p;
+    std::memcpy(m->lds_blob_layout, layout, sizeof layout);
+    return p;
 }
 
 void copy_scalars(rg_scene *dst, const rg_scene *src) {

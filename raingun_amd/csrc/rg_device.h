@@ -177,6 +177,9 @@ struct RgKernelArgs {
     // the 4 statistics words (rays by class, error key) there -- no copy after the kernel
     unsigned long long *snap_out;
     uint32_t max_grid_threads;  // nonzero: cap on the persistent grid (the deep frame buffer's memory bound)
+    // nullable: the whole LDS arena [0, lds_total_bytes) as one device image (light path): a
+    // block stages its scene copy with ONE unrolled loop instead of a loop per table
+    const void *lds_blob;
 };
 
 __host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }

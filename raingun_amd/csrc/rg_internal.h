@@ -170,6 +170,10 @@ struct rg_scene {
     int multi_bands = 0;
     int multi_only_rank = -1;  // stand-in direct mode: issue only this device's work (timeline rehearsal)
     std::shared_ptr<const rg_host_tables> host;
+    std::vector<RgTexDev> tex_desc;  // the uploaded texture descriptors (device texel pointers)
+    // the LDS arena as one device image (RgKernelArgs::lds_blob), for the layout it was built for
+    void *lds_blob = nullptr;
+    uint32_t lds_blob_layout[14] = {};
     mutable std::vector<rg_launch_ctx *> ctxs;  // one per stream used
     mutable rg_launch_ctx *last = nullptr;       // the context of the latest launch (rg_debug_counters)
     mutable rg_image_res img;

@@ -1432,7 +1432,29 @@ void rg_render_kernel(RgKernelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     typename std::conditional<LSPH, SphLds, SphScalar>::type src;
     Cold T;
+    // light path: every one-wave block stages its own copy of the (few-KB) scene; with the
+    // arena's device image that is one loop with all its loads in flight at once
+    const bool blob = LB > 1 && LSPH && LCOLD && a.lds_blob != nullptr;
+    if (blob) {
+        const uint4 *g = reinterpret_cast<const uint4 *>(a.lds_blob);
+        uint4 *d = reinterpret_cast<uint4 *>(smem);
+        const uint32_t n16 = a.lds_total_bytes / 16u;
+        for (uint32_t k0 = threadIdx.x; k0 < n16; k0 += 4u * blockDim.x) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + (uint32_t)u * blockDim.x;
+                if (k < n16) v[u] = g[k];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + (uint32_t)u * blockDim.x;
+                if (k < n16) d[k] = v[u];
+            }
+        }
+    }
     if constexpr (LSPH) {
+        if (!blob) {
         stage16(smem + a.lds_sphf, a.sphf, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF));
         stage16(smem + a.lds_sphf + (size_t)a.n_sph * sizeof(RgSphF), a.sphf2, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSphF2));
         stage16(smem + a.lds_sph, a.sph, (uint32_t)a.n_sph * (uint32_t)sizeof(RgSph));
@@ -1443,6 +1465,7 @@ void rg_render_kernel(RgKernelArgs a) {
         stage16(smem + a.lds_pln, a.pln, (uint32_t)a.n_pln * (uint32_t)sizeof(RgPln));
         stage16(smem + a.lds_dsk, a.dsk, (uint32_t)a.n_dsk * (uint32_t)sizeof(RgDsk));
         stage16(smem + a.lds_box, a.box, a.lds_bodies - a.lds_box);
+        }
         src.f = reinterpret_cast<const RgSphF *>(smem + a.lds_sphf);
         src.f2 = reinterpret_cast<const RgSphF2 *>(smem + a.lds_sphf + (size_t)a.n_sph * sizeof(RgSphF));
         src.s = reinterpret_cast<const RgSph *>(smem + a.lds_sph);
@@ -1465,10 +1488,12 @@ void rg_render_kernel(RgKernelArgs a) {
         src.nd = rg_cptr(a.nodes);
     }
     if constexpr (LCOLD) {
-        stage16(smem + a.lds_bodies, a.bodies, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgBodyDev));
-        stage16(smem + a.lds_mats, a.mats, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgMatDev));
-        stage16(smem + a.lds_lights, a.lights, (uint32_t)a.n_lights * (uint32_t)sizeof(RgLightDev));
-        stage16(smem + a.lds_texs, a.texs, (uint32_t)a.n_textures * (uint32_t)sizeof(RgTexDev));
+        if (!blob) {
+            stage16(smem + a.lds_bodies, a.bodies, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgBodyDev));
+            stage16(smem + a.lds_mats, a.mats, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgMatDev));
+            stage16(smem + a.lds_lights, a.lights, (uint32_t)a.n_lights * (uint32_t)sizeof(RgLightDev));
+            stage16(smem + a.lds_texs, a.texs, (uint32_t)a.n_textures * (uint32_t)sizeof(RgTexDev));
+        }
         T.bodies = reinterpret_cast<const RgBodyDev *>(smem + a.lds_bodies);
         T.mats = reinterpret_cast<const RgMatDev *>(smem + a.lds_mats);
         T.lights = reinterpret_cast<const RgLightDev *>(smem + a.lds_lights);
