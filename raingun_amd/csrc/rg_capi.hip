@@ -235,7 +235,8 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
     const bool lane = bvh && rg_heavy_path(a) && s->lane_stack > 0 && s->lane_min_depth < 1 << 20;
     a.lane_stack = lane ? s->lane_stack : 0;
     a.lane_min_depth = lane ? s->lane_min_depth : 1 << 30;
-    a.lds_lstack_bytes = (uint32_t)a.lane_stack * 256u * RG_HEAVY_WPS * 4u;
+    // lane_stack entries + one spare slot per lane (rg_kernels.hip bvh_lane, RG_LANE_BRANCHFREE)
+    a.lds_lstack_bytes = lane ? (uint32_t)(a.lane_stack + 1) * 256u * RG_HEAVY_WPS * 4u : 0u;
     // LDS arena: [lane stacks | sphf | sphf2 | sph | cc (padded to 16 B) | nodes | pln | dsk | box (padded) |
     //             bodies | mats | lights | texs]
     auto al16 = [](uint32_t v) { return (v + 15u) & ~15u; };

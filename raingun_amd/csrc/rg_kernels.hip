@@ -601,6 +601,9 @@ __device__ __forceinline__ void cswap(uint32_t &x, uint32_t &y) {
     y = hi;
 }
 
+#ifndef RG_LANE_BRANCHFREE
+#define RG_LANE_BRANCHFREE 1  // per-lane walk: child slots processed without divergent branches (one spare stack slot)
+#endif
 #ifndef RG_LANE_LEAF_BATCH
 #define RG_LANE_LEAF_BATCH 0  // 1: the per-lane walk postpones leaf tests and runs them in batches (below)
 #endif
@@ -708,6 +711,54 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             }
         }
 #endif
+#if RG_LANE_BRANCHFREE
+        if (act) {
+            // the node's children without divergent branches: every slot's slab test,
+            // hit leaves as a bit mask (tested below in child order), hit internal
+            // children as sort keys (~0: none), pushes written unconditionally
+            const RgBvhNode N = src.getn(node);
+            const float tb = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
+            uint32_t e[4], leaves = 0u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float tn = 0.0f;
+                const bool h = (k < N.nchild) & rg_child_hit(N, k, rb, tb, tn);
+                const int ch = N.child[k];
+                leaves |= (h & (ch < 0)) ? (1u << k) : 0u;
+                e[k] = (h & (ch >= 0)) ? lane_key(tn, ch) : ~0u;
+            }
+            // leaves first (they tighten a closest-hit bound), in child order
+            while (leaves != 0u && need) {
+                const uint32_t k = (uint32_t)__builtin_ctz(leaves);
+                leaves &= leaves - 1u;
+                const int v = ~(k == 0u ? N.child[0] : k == 1u ? N.child[1] : k == 2u ? N.child[2] : N.child[3]);
+                leaf_query(a, src, v >> 3, (v & 7) + 1, o, d, rf, shadow, ld, c, occl, need);
+            }
+            uint32_t e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
+            // ascending (entry distance, node); empty slots (~0) last
+            cswap(e0, e1); cswap(e2, e3); cswap(e0, e2); cswap(e1, e3); cswap(e1, e2);
+            // slot `cap` is a spare: a write that is not a push may land there, never on an entry
+            stk[(uint32_t)min(sp, cap) * stride] = e3;
+            sp += (e3 != ~0u) & (sp < cap);
+            stk[(uint32_t)min(sp, cap) * stride] = e2;
+            sp += (e2 != ~0u) & (sp < cap);
+            stk[(uint32_t)min(sp, cap) * stride] = e1;
+            sp += (e1 != ~0u) & (sp < cap);
+            const float tbn = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
+            if (e0 != ~0u && (shadow || !(lane_key_t(e0) > tbn))) {
+                node = (int)(e0 & mask);
+            } else {
+                node = -1;
+                while (sp > 0 && need) {
+                    const uint32_t e = stk[(uint32_t)(--sp) * stride];
+                    if (shadow || !(lane_key_t(e) > tbn)) {
+                        node = (int)(e & mask);
+                        break;
+                    }
+                }
+            }
+        }
+#else
         if (act) {
             const RgBvhNode N = src.getn(node);
             const float tb = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
@@ -769,6 +820,7 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
                 }
             }
         }
+#endif
     }
 #endif
     RG_STAT(12, RG_CLOCK() - t_in);
@@ -2598,7 +2650,8 @@ extern "C" hipError_t rg_render_grid_threads(const RgKernelArgs *a, int maxd, si
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,
                                       int32_t *body, hipStream_t stream) {
     dim3 grid((n + 255) / 256);
-    const size_t lds = (size_t)a->lane_stack * 256u * 4u;  // per-lane walk stacks (stride = block size)
+    // per-lane walk stacks (stride = block size): lane_stack entries + the spare slot
+    const size_t lds = a->lane_stack > 0 ? (size_t)(a->lane_stack + 1) * 256u * 4u : 0u;
     hipLaunchKernelGGL(rg_trace_kernel, grid, dim3(256), lds, stream, *a, rays, n, dist, body);
     return hipGetLastError();
 }
