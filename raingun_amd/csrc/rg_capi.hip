@@ -669,7 +669,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         md.tex = m.texture;
         md.xoff = m.x_offset;
         md.yoff = m.y_offset;
-        md.albedo = m.albedo;
+        md.albedo_pi = m.albedo / 3.14159265358979323846f;  // std::f32::consts::PI, IEEE f32 division
         md.surface = (int32_t)m.surface;
         md.reflectivity = m.reflectivity;
         md.index = m.index;

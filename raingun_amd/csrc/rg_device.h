@@ -73,7 +73,7 @@ struct RgMatDev {          // material.rs:66-71, flattened
     float color[3];
     int32_t tex;
     float xoff, yoff;
-    float albedo;
+    float albedo_pi;       // albedo / f32::consts::PI (rendering.rs:164), the host's f32 division
     int32_t surface;
     float reflectivity;
     float index;

@@ -1680,7 +1680,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             // no hit-point state (h, n, incident) has to survive the shadow pass
                             const C3 col = surface_color(T.texs, m, b, h);
                             park[64 * PK_COL] = col.r; park[64 * (PK_COL + 1)] = col.g; park[64 * (PK_COL + 2)] = col.b;
-                            park[64 * PK_REFL] = m.albedo / PI_F;                   // rendering.rs:164
+                            park[64 * PK_REFL] = m.albedo_pi;                       // rendering.rs:164
                             // how the batch's colour is used: 0 diffuse, 1 reflecting at the depth
                             // limit (mix with the default colour), 2 reflecting with a frame
                             const int kind = m.surface == RG_SURFACE_DIFFUSE ? 0 : qdepth + 1 < max_depth ? 2 : 1;
@@ -1830,7 +1830,7 @@ void rg_render_kernel(RgKernelArgs a) {
                 // shade_diffuse loop body (rendering.rs:141-170), one light per iteration
                 const RgMatDev m = T.mats[hb];
                 if (rmode == MODE_SHADOW) {
-                    const float refl = m.albedo / PI_F;
+                    const float refl = m.albedo_pi;  // albedo / PI (rendering.rs:164)
 #pragma unroll
                     for (int l = 0; l < LB; ++l) {
                         if (li + l < a.n_lights) {
