@@ -176,10 +176,11 @@ def roofline(key: str, frame_s: float, n_gpus: int, alg_bytes: int, tex: int, al
     if w:
         cyc = w["valu_cycles_per_frame"]
         frac = cyc / (frame_s * n_gpus * SIMDS * CLOCK_HZ)
-        c = w.get("counters_per_frame", {})
-        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:  # KiB per frame as collected
-            res["traffic_raw"] = {"fetch_size_bytes": round(c["FETCH_SIZE"] * 1024), "write_size_bytes":
-                                  round(c["WRITE_SIZE"] * 1024), "fetch_correction": "x2 in traffic (gfx950)"}
+        fw = w.get("fetch_write_kib_per_frame")  # PMC FETCH_SIZE, WRITE_SIZE (KiB per frame as collected)
+        if fw and None not in fw:
+            res["traffic_raw"] = {"fetch_size_bytes": round(fw[0] * 1024), "write_size_bytes": round(fw[1] * 1024),
+                                  "note": "uncorrected; `traffic` doubles FETCH (gfx950 correction for wide "
+                                          "streaming reads, unvalidated for scratch/texel/table reads)"}
         res.update({
             "achieved": round(cyc * 16.0 / frame_s / 1e12, 4),
             "frac": round(frac, 5),

@@ -84,7 +84,7 @@ void make_filter_records(const double *p, RgSphF &f, RgSphF2 &f2) {
     f2.cc32 = (float)cc;
     const double kd1 = u * (16.2 + 26.2 * 1.00001) * 1.01;  // primary rays: |o| = 0, |d|^2 <= 1.00001
     f2.thrp = f32_up(((double)f.r2hi + kd1 * (double)f2.cchi) * (1.0 + 1e-6));
-    f2.pad = 0.0f;
+    f2.id = -1;  // set with sph_id
 }
 
 // f64::to_radians (2017 std: self * (PI / 180)), then libm tan (ray.rs:45).
@@ -682,6 +682,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
             h.sphf.emplace_back();
             h.sphf2.emplace_back();
             make_filter_records(p, h.sphf.back(), h.sphf2.back());
+            h.sphf2.back().id = (int32_t)i;  // the record a leaf test already holds carries the id
             h.sph_cc.push_back(dot3(p, p));  // padded to an even count after the loop
             h.sph_id.push_back((int32_t)i);
             sph_raw.insert(sph_raw.end(), p, p + 4);

@@ -38,7 +38,7 @@ struct alignas(16) RgSph { double cx, cy, cz, r2; };
 // f32 pre-filter records (see rg_kernels.hip, "f32 pre-filter"): conservative
 // bounds, never values the exact test uses.
 struct alignas(16) RgSphF { float cx, cy, cz, r2hi; };       // c rounded to f32; r2 rounded up (+slack)
-struct alignas(16) RgSphF2 { float cchi, thrp, cc32, pad; };  // |c|^2 rounded up; primary-ray threshold; fl32(c.c)
+struct alignas(16) RgSphF2 { float cchi, thrp, cc32; int32_t id; };  // |c|^2 rounded up; primary-ray threshold; fl32(c.c); YAML body id (= sph_id)
 struct alignas(16) RgPln { double ox, oy, oz, nx, ny, nz, on, pad; };
 struct alignas(16) RgDsk { double ox, oy, oz, nx, ny, nz, r, on; };
 struct alignas(16) RgBox { double lo[3], hi[3]; };

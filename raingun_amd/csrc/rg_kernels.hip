@@ -466,13 +466,14 @@ template <class Src>
 __device__ __forceinline__ void leaf_primary(const RgKernelArgs &a, const Src &src, int first, int count, V3 d,
                                              float dx, float dy, float dz, Closest &c) {
     for (int j = first; j < first + count; ++j) {
-        if (filter_primary(src.getf(j), src.getf2(j), dx, dy, dz)) {
+        const RgSphF2 f2 = src.getf2(j);
+        if (filter_primary(src.getf(j), f2, dx, dy, dz)) {
             const RgSph s = src.get(j);
             const double cc = src.getcc(j);
             const double adj = (s.cx * d.x + s.cy * d.y) + s.cz * d.z;
             const double opp = cc - adj * adj;
             double t;
-            if (!(opp > s.r2) && sphere_tail(s.r2, opp, adj, t)) closest_add(c, t, rg_cptr(a.sph_id)[j]);
+            if (!(opp > s.r2) && sphere_tail(s.r2, opp, adj, t)) closest_add(c, t, f2.id);
         }
     }
 }
@@ -482,7 +483,10 @@ __device__ __forceinline__ void leaf_query(const RgKernelArgs &a, const Src &src
                                            const RayF &rf, bool shadow, double ld, Closest &c, bool &occl,
                                            bool &need) {
     for (int j = first; j < first + count; ++j) {
-        if (need && filter_general(src.getf(j), src.getf2(j), rf)) {
+        // the id comes with the filter record (RgSphF2::id): a per-lane j (bvh_lane) would
+        // otherwise make sph_id[j] a vector global load whose latency the hit waits for
+        const RgSphF2 f2 = src.getf2(j);
+        if (need && filter_general(src.getf(j), f2, rf)) {
             const RgSph s = src.get(j);
             const double hx = s.cx - o.x, hy = s.cy - o.y, hz = s.cz - o.z;
             const double adj = (hx * d.x + hy * d.y) + hz * d.z;
@@ -492,7 +496,7 @@ __device__ __forceinline__ void leaf_query(const RgKernelArgs &a, const Src &src
                 if (shadow) {
                     if (!(t > ld)) { occl = true; need = false; }
                 } else {
-                    closest_add(c, t, rg_cptr(a.sph_id)[j]);
+                    closest_add(c, t, f2.id);
                 }
             }
         }
@@ -619,7 +623,8 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
     const RayB rb = rg_make_rayb(ob.x, ob.y, ob.z, d.x, d.y, d.z);
     const RayF rf = make_rayf(o, d);
     const float tld = shadow ? bvh_bound(ld - t0s) : 0.0f;
-    int node = 0, sp = 0;
+    int node = 0;
+    [[maybe_unused]] int sp = 0;
     RG_STAT(4, 1);
     RG_STAT(7, RG_LANES(1));
     [[maybe_unused]] const unsigned long long t_in = RG_CLOCK();
@@ -698,6 +703,10 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
         }
     }
 #else
+#if RG_LANE_BRANCHFREE
+    const uint32_t capo = (uint32_t)cap * stride;
+    uint32_t spo = 0u;
+#endif
     for (;;) {
         const bool act = need && node >= 0;
         if (!__any(act)) break;
@@ -737,20 +746,22 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             uint32_t e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
             // ascending (entry distance, node); empty slots (~0) last
             cswap(e0, e1); cswap(e2, e3); cswap(e0, e2); cswap(e1, e3); cswap(e1, e2);
-            // slot `cap` is a spare: a write that is not a push may land there, never on an entry
-            stk[(uint32_t)min(sp, cap) * stride] = e3;
-            sp += (e3 != ~0u) & (sp < cap);
-            stk[(uint32_t)min(sp, cap) * stride] = e2;
-            sp += (e2 != ~0u) & (sp < cap);
-            stk[(uint32_t)min(sp, cap) * stride] = e1;
-            sp += (e1 != ~0u) & (sp < cap);
+            // slot `cap` is a spare: a write that is not a push may land there, never on an entry;
+            // the stack pointer is kept scaled by the stride (spo = sp * stride: no multiplies)
+            stk[min(spo, capo)] = e3;
+            spo += ((e3 != ~0u) & (spo < capo)) ? stride : 0u;
+            stk[min(spo, capo)] = e2;
+            spo += ((e2 != ~0u) & (spo < capo)) ? stride : 0u;
+            stk[min(spo, capo)] = e1;
+            spo += ((e1 != ~0u) & (spo < capo)) ? stride : 0u;
             const float tbn = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
             if (e0 != ~0u && (shadow || !(lane_key_t(e0) > tbn))) {
                 node = (int)(e0 & mask);
             } else {
                 node = -1;
-                while (sp > 0 && need) {
-                    const uint32_t e = stk[(uint32_t)(--sp) * stride];
+                while (spo > 0u && need) {
+                    spo -= stride;
+                    const uint32_t e = stk[spo];
                     if (shadow || !(lane_key_t(e) > tbn)) {
                         node = (int)(e & mask);
                         break;

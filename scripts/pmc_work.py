@@ -115,6 +115,7 @@ def main():
         work[f"{wl}@{size}"] = {k: d[k] for k in ("valu_insts_per_frame", "f64_insts_per_frame",
                                                   "trans32_insts_per_frame", "valu_cycles_per_frame",
                                                   "hbm_bytes_per_frame", "source")}
+        work[f"{wl}@{size}"]["fetch_write_kib_per_frame"] = [a.get("FETCH_SIZE"), a.get("WRITE_SIZE")]
         print(tag, json.dumps({k: v for k, v in d.items() if k != "counters_per_frame"}, indent=1))
     out_f.write_text(json.dumps(work, indent=1, sort_keys=True) + "\n")
 
