@@ -1152,6 +1152,15 @@ __device__ __forceinline__ uint32_t wrap(float v, int32_t max) {
 }
 
 // material.rs:115-148 + color.rs:26-30
+// (float)b / 255.0f for a byte b (material.rs Texture::color, color.rs from_rgba), correctly
+// rounded: one multiply and a residual correction instead of the IEEE division expansion.  Equal to
+// the division for every one of the 256 inputs (checked exhaustively: tests/test_primitives_kat.py).
+__device__ __forceinline__ float u8_div255(uint32_t b) {
+    const float x = (float)b, inv = 1.0f / 255.0f;
+    const float q0 = x * inv;
+    return __builtin_fmaf(__builtin_fmaf(-q0, 255.0f, x), inv, q0);
+}
+
 __device__ __forceinline__ C3 material_color(const RgTexDev *texs, const RgMatDev &m, float tx, float ty) {
     if (m.coloration == RG_COLORATION_COLOR) return c3(m.color[0], m.color[1], m.color[2]);
 #ifdef RG_DBG_NO_TEX  // timing ablation only (wrong images)
@@ -1160,9 +1169,10 @@ __device__ __forceinline__ C3 material_color(const RgTexDev *texs, const RgMatDe
     const RgTexDev t = texs[m.tex];
     uint32_t x = wrap(tx + m.xoff, t.w);
     uint32_t y = wrap(ty + m.yoff, t.h);
-    uint32_t px = t.texels[(size_t)y * (uint32_t)t.w + x];
-    return c3((float)(px & 0xffu) / 255.0f, (float)((px >> 8) & 0xffu) / 255.0f,
-              (float)((px >> 16) & 0xffu) / 255.0f);
+    // texels live in global memory: a global (not flat) load, so its wait does not also drain LDS
+    const __attribute__((address_space(1))) uint32_t *tg = (const __attribute__((address_space(1))) uint32_t *)t.texels;
+    uint32_t px = tg[(size_t)y * (uint32_t)t.w + x];
+    return c3(u8_div255(px & 0xffu), u8_div255((px >> 8) & 0xffu), u8_div255((px >> 16) & 0xffu));
 }
 
 // body.color(&body.texture_coords(hit)) (rendering.rs:134-135, 103).  The

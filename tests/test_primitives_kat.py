@@ -103,3 +103,23 @@ def test_depth_zero_still_shades_primary(oracle_lib, example_scenes):
     s.max_recursion_depth = 0
     _, rgba, _, counts, _ = oracle_lib.render(SceneDesc(s), 80, 60)
     assert counts["primary"] == 4800 and counts["secondary"] == 0 and counts["shadow"] > 0
+
+
+def test_u8_div255_residual_form_is_exact(tmp_path):
+    """The kernel converts texel bytes with q0 = b * (1/255); q = fma(fma(-q0, 255, b), 1/255, q0)
+    (rg_kernels.hip u8_div255) instead of the IEEE division the reference does (b as f32 / 255.0).
+    Check, for all 256 byte values, that both give the same f32 (C fmaf, no contraction)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    src = tmp_path / "div255.c"
+    src.write_text(
+        "#include <math.h>\n#include <stdio.h>\n"
+        "int main(void){const float inv=1.0f/255.0f;int bad=0;for(int b=0;b<256;++b){float x=(float)b;"
+        "volatile float d=255.0f;float q=x/d;float q0=x*inv;float q1=fmaf(fmaf(-q0,255.0f,x),inv,q0);"
+        "if(q1!=q)++bad;}printf(\"%d\\n\",bad);return 0;}\n")
+    exe = tmp_path / "div255"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(src), "-lm"], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.strip()
+    assert out == "0"
