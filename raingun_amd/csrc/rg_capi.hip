@@ -238,7 +238,9 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
     // lane_stack entries + one spare slot per lane (rg_kernels.hip bvh_lane, RG_LANE_BRANCHFREE)
     a.lds_lstack_bytes = lane ? (uint32_t)(a.lane_stack + 1) * 256u * RG_HEAVY_WPS * 4u : 0u;
     // LDS arena: [lane stacks | sphf | sphf2 | sph | cc (padded to 16 B) | nodes | pln | dsk | box (padded) |
-    //             bodies | mats | lights | texs]
+    //             lights | texs (padded) | bodies | mats].  The hot part (staged whenever the sphere
+    //             tables are) ends after the texture descriptors: lights and texture descriptors are a
+    //             few hundred bytes that every shadow ray / textured hit reads with a per-lane index.
     auto al16 = [](uint32_t v) { return (v + 15u) & ~15u; };
     a.lds_sphf = a.lds_lstack_bytes;
     a.lds_sph = a.lds_sphf + (uint32_t)s->n_sph * (uint32_t)(sizeof(RgSphF) + sizeof(RgSphF2));
@@ -247,12 +249,12 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
     a.lds_pln = a.lds_nodes + (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode);
     a.lds_dsk = a.lds_pln + (uint32_t)s->n_pln * (uint32_t)sizeof(RgPln);
     a.lds_box = a.lds_dsk + (uint32_t)s->n_dsk * (uint32_t)sizeof(RgDsk);
-    a.lds_bodies = al16(a.lds_box + (uint32_t)s->n_box * (uint32_t)sizeof(RgBox));
+    a.lds_lights = al16(a.lds_box + (uint32_t)s->n_box * (uint32_t)sizeof(RgBox));
+    a.lds_texs = a.lds_lights + (uint32_t)s->n_lights * (uint32_t)sizeof(RgLightDev);
+    a.lds_bodies = al16(a.lds_texs + (uint32_t)s->n_textures * (uint32_t)sizeof(RgTexDev));
     a.lds_hot_bytes = a.lds_bodies;
     a.lds_mats = a.lds_bodies + (uint32_t)s->n_bodies * (uint32_t)sizeof(RgBodyDev);
-    a.lds_lights = al16(a.lds_mats + (uint32_t)s->n_bodies * (uint32_t)sizeof(RgMatDev));
-    a.lds_texs = a.lds_lights + (uint32_t)s->n_lights * (uint32_t)sizeof(RgLightDev);
-    a.lds_total_bytes = a.lds_texs + (uint32_t)s->n_textures * (uint32_t)sizeof(RgTexDev);
+    a.lds_total_bytes = a.lds_mats + (uint32_t)s->n_bodies * (uint32_t)sizeof(RgMatDev);
     a.def[0] = s->def[0];
     a.def[1] = s->def[1];
     a.def[2] = s->def[2];

@@ -1487,8 +1487,8 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // Render kernel.  Heavy path: ONE persistent block of 256*WPS threads per CU
 // (WPS waves per SIMD).  Light path: one-wave blocks, each rendering at most
 // RG_LIGHT_TILES_PER_WAVE tiles (launcher: launch_one).  A block stages the
-// scene into LDS (LSPH: sphere tables; LCOLD: bodies, materials, lights,
-// texture descriptors), then every wave repeatedly takes the next 8x8 pixel
+// scene into LDS (LSPH: sphere, plane, disk and box tables, lights, texture
+// descriptors; LCOLD: bodies, materials), then every wave repeatedly takes the next 8x8 pixel
 // tile from an atomic queue (counters[16..], sharded) and runs the per-lane
 // state machine until its 64 lanes have written their pixels.
 template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
@@ -1537,7 +1537,9 @@ void rg_render_kernel(RgKernelArgs a) {
         }
         stage16(smem + a.lds_pln, a.pln, (uint32_t)a.n_pln * (uint32_t)sizeof(RgPln));
         stage16(smem + a.lds_dsk, a.dsk, (uint32_t)a.n_dsk * (uint32_t)sizeof(RgDsk));
-        stage16(smem + a.lds_box, a.box, a.lds_bodies - a.lds_box);
+        stage16(smem + a.lds_box, a.box, a.lds_lights - a.lds_box);
+        stage16(smem + a.lds_lights, a.lights, (uint32_t)a.n_lights * (uint32_t)sizeof(RgLightDev));
+        stage16(smem + a.lds_texs, a.texs, a.lds_bodies - a.lds_texs);
         }
         src.f = reinterpret_cast<const RgSphF *>(smem + a.lds_sphf);
         src.f2 = reinterpret_cast<const RgSphF2 *>(smem + a.lds_sphf + (size_t)a.n_sph * sizeof(RgSphF));
@@ -1564,16 +1566,17 @@ void rg_render_kernel(RgKernelArgs a) {
         if (!blob) {
             stage16(smem + a.lds_bodies, a.bodies, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgBodyDev));
             stage16(smem + a.lds_mats, a.mats, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgMatDev));
-            stage16(smem + a.lds_lights, a.lights, (uint32_t)a.n_lights * (uint32_t)sizeof(RgLightDev));
-            stage16(smem + a.lds_texs, a.texs, (uint32_t)a.n_textures * (uint32_t)sizeof(RgTexDev));
         }
         T.bodies = reinterpret_cast<const RgBodyDev *>(smem + a.lds_bodies);
         T.mats = reinterpret_cast<const RgMatDev *>(smem + a.lds_mats);
-        T.lights = reinterpret_cast<const RgLightDev *>(smem + a.lds_lights);
-        T.texs = reinterpret_cast<const RgTexDev *>(smem + a.lds_texs);
     } else {
         T.bodies = a.bodies;
         T.mats = a.mats;
+    }
+    if constexpr (LSPH) {  // lights and texture descriptors: part of the hot tables
+        T.lights = reinterpret_cast<const RgLightDev *>(smem + a.lds_lights);
+        T.texs = reinterpret_cast<const RgTexDev *>(smem + a.lds_texs);
+    } else {
         T.lights = a.lights;
         T.texs = a.texs;
     }
