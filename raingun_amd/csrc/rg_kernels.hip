@@ -1118,9 +1118,8 @@ __device__ __attribute__((noinline))
 #else
 __device__ __forceinline__
 #endif
-void sphere_uv(double hx, double hy, double hz, double r, float &tx, float &ty) {
-    tx = (1.0f + ((float)atan2(hz, hx)) / PI_F) * 0.5f;
-    ty = ((float)acos(hy / r)) / PI_F;
+float2 sphere_uv(double hx, double hy, double hz, double r) {  // returned in VGPRs (no scratch round trip)
+    return make_float2((1.0f + ((float)atan2(hz, hx)) / PI_F) * 0.5f, ((float)acos(hy / r)) / PI_F);
 }
 
 // bodies.rs:126-132, 155-169, 198-212, 330-333
@@ -1130,7 +1129,9 @@ __device__ __forceinline__ void texture_coords(const RgBodyDev &b, V3 h, float &
 #ifdef RG_DBG_NO_ATAN  // timing ablation only (wrong images)
         tx = (float)hv.x; ty = (float)hv.y; return;
 #endif
-        sphere_uv(hv.x, hv.y, hv.z, b.p[3], tx, ty);
+        const float2 uv = sphere_uv(hv.x, hv.y, hv.z, b.p[3]);
+        tx = uv.x;
+        ty = uv.y;
     } else if (b.kind == RG_BODY_AABB) {
         tx = 0.0f;
         ty = 0.0f;
@@ -1512,18 +1513,16 @@ void rg_render_kernel(RgKernelArgs a) {
         const uint4 *g = reinterpret_cast<const uint4 *>(a.lds_blob);
         uint4 *d = reinterpret_cast<uint4 *>(smem);
         const uint32_t n16 = a.lds_total_bytes / 16u;
+        // four loads in flight per lane: unconditional (indices clamped into the image), then
+        // the guarded LDS stores -- no per-lane array, which hipcc placed in scratch
+        const uint32_t last = n16 - 1u;
         for (uint32_t k0 = threadIdx.x; k0 < n16; k0 += 4u * blockDim.x) {
-            uint4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t k = k0 + (uint32_t)u * blockDim.x;
-                if (k < n16) v[u] = g[k];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t k = k0 + (uint32_t)u * blockDim.x;
-                if (k < n16) d[k] = v[u];
-            }
+            const uint32_t k1 = k0 + blockDim.x, k2 = k1 + blockDim.x, k3 = k2 + blockDim.x;
+            const uint4 v0 = g[k0], v1 = g[min(k1, last)], v2 = g[min(k2, last)], v3 = g[min(k3, last)];
+            d[k0] = v0;
+            if (k1 < n16) d[k1] = v1;
+            if (k2 < n16) d[k2] = v2;
+            if (k3 < n16) d[k3] = v3;
         }
     }
     if constexpr (LSPH) {
