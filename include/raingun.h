@@ -258,16 +258,20 @@ rg_status rg_trace(const rg_scene *scene, const double *rays, uint32_t n,
  * rg_render_image, split over `ngpus` devices -- the scene's device first,
  * then the next visible devices in order -- in `tile_rows`-row tiles dealt
  * round-robin (tile t -> device t % ngpus; 0 = 8 rows).  Each device renders
- * its tiles with its own replica of the scene (made on first use and kept),
- * ONE RCCL ncclGather over xGMI brings the equal-size parts to the scene's
- * device, which re-interleaves them into the frame; the frame is then copied
- * to `rgba_out` (width*height*4 bytes, host).  The communicators come from
- * ncclCommInitAll in this process (RCCL is loaded at run time: the librccl
- * already in the process, else $RG_RCCL_LIBRARY, else librccl.so.1);
- * RG_ERR_COLLECTIVE if it cannot be loaded.  No torch, no launcher: the
- * drop-in for the reference's one blocking call (rendering.rs:24-38,
- * src/render.rs:55) on a whole node.  `stats` sums the devices' rays;
- * kernel_ms spans render + gather + assembly. */
+ * its tiles with its own replica of the scene (made on first use and kept)
+ * in row bands, and after each band copies that band's tiles straight to
+ * their image rows of `rgba_out` (width*height*4 bytes, host) with one
+ * strided copy over its OWN PCIe link, overlapped with its later bands: N
+ * links carry 1/N of the frame each (a pageable buffer is fed from a pinned
+ * frame by host threads).  The RCCL path -- one ncclGather over xGMI to the
+ * scene's device, re-interleave, one copy -- remains available through
+ * rg_debug_set_multi (mode 1); its communicators come from ncclCommInitAll in
+ * this process (RCCL loaded at run time: the librccl already in the process,
+ * else $RG_RCCL_LIBRARY, else librccl.so.1; RG_ERR_COLLECTIVE if it cannot be
+ * loaded).  No torch, no launcher: the drop-in for the reference's one
+ * blocking call (rendering.rs:24-38, src/render.rs:55) on a whole node.
+ * `stats` sums the devices' rays; on device errors error_pixel is the lowest
+ * failing pixel of any device; kernel_ms spans the whole call. */
 rg_status rg_render_multi(const rg_scene *scene, uint32_t width, uint32_t height, int32_t ngpus,
                           uint32_t tile_rows, uint8_t *rgba_out, rg_stats *stats);
 
