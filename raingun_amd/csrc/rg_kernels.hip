@@ -39,7 +39,7 @@ constexpr float PI_F = 3.14159265358979323846f;       // std::f32::consts::PI
 enum : int { MODE_CLOSEST = 0, MODE_SHADOW = 1, MODE_DONE = 2, MODE_WAIT = 3, MODE_SHADOW_H = 4 };
 // MODE_SHADOW_H: an idle lane tracing one shadow ray for another lane of its wave (shadow fan-out)
 // FR_REFR_TASK / FR_REFR_WAIT carry their pool slot in bits 8+ of Frame::type
-enum : int { FR_REFL = 0, FR_REFR_T = 1, FR_REFR_R = 2, FR_REFL_PEND = 3, FR_REFR_TASK = 4, FR_REFR_WAIT = 5 };
+enum : int { FR_REFL = 0, FR_REFR_T = 1, FR_REFR_R = 2, FR_REFR_TASK = 4, FR_REFR_WAIT = 5 };
 
 struct V3 { double x, y, z; };
 struct C3 { float r, g, b; };
@@ -1261,7 +1261,8 @@ struct Frame {
     float f[8];   // REFL: D.rgb, r.  REFR: kr, tau, surf.rgb, Tc.rgb
     double rr[6]; // REFR_T: pending reflection ray (origin, direction)
     int type;
-    int cdepth;   // depth of this node's children
+    int cdepth;   // depth of this node's children (task-splitting kernels only: elsewhere a lane's
+                  // stack index IS its recursion depth, so frame sp-1's children are at depth sp)
 };
 
 // The lane's stack of open frames: at most max_recursion_depth - 1 deep
@@ -1639,7 +1640,7 @@ void rg_render_kernel(RgKernelArgs a) {
     uint32_t occl_full = 0u;
     int qdepth = 0;        // closest: depth of the ray
     // hit being shaded
-    V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0), hd = v3(0, 0, 0);
+    V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0);
     int hb = 0, hdepth = 0, li = 0;
     int nfan = 0;              // shadow fan-out: lights li+1 .. li+nfan of this hit traced by helper lanes
     uint32_t fan_lanes = 0u;   // ... their lanes, 6 bits each
@@ -1714,13 +1715,8 @@ void rg_render_kernel(RgKernelArgs a) {
                             // by the shadow pass) carries the reflection direction until the
                             // batch is shaded -- the frame holds only colour state
                             q.o = add(h, scl(n, SHADOW_BIAS));
-                            if (m.surface == RG_SURFACE_REFLECTING && qdepth + 1 < max_depth) {
-                                Frame &f = stk[sp++];                               // rendering.rs:88,
-                                f.type = FR_REFL_PEND;                              // D filled in later
-                                f.f[3] = m.reflectivity;
-                                f.cdepth = qdepth + 1;
-                                q.d = sub(q.d, scl(n, 2.0 * dot(q.d, n)));          // ray.rs:58
-                            }
+                            // (rendering.rs:88: its frame is pushed once the batch is shaded)
+                            if (kind == 2) q.d = sub(q.d, scl(n, 2.0 * dot(q.d, n)));  // ray.rs:58
                             occl_full = 0u;
 #pragma unroll
                             for (int l = 0; l < LB; ++l) {
@@ -1742,7 +1738,12 @@ void rg_render_kernel(RgKernelArgs a) {
                             bcol = surface_color(T.texs, m, b, h);
                             hb = c.id; hdepth = qdepth;
                             fin = c3(0.0f, 0.0f, 0.0f);
-                            hp = h; hn = n; hd = q.d; li = 0;
+                            hp = h; hn = n; li = 0;
+                            // a reflecting hit's reflection direction (ray.rs:58) goes into q.d
+                            // now -- the shadow queries use q.o and sb only -- so the incident
+                            // direction does not stay live across the light loop
+                            if (m.surface == RG_SURFACE_REFLECTING && qdepth + 1 < max_depth)
+                                q.d = sub(q.d, scl(n, 2.0 * dot(q.d, n)));
                             shade = true;
                         }
                     } else {
@@ -1760,7 +1761,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             Frame &f = stk[sp++];
                             f.f[0] = kr; f.f[1] = m.transparency;
                             f.f[2] = surf.r; f.f[3] = surf.g; f.f[4] = surf.b;
-                            f.cdepth = cd;
+                            if constexpr (TASKS) f.cdepth = cd;
                             // rendering.rs:100-113: the transmission subtree is traced first while
                             // the reflection ray (ray.rs:56-60) waits in the frame or, with task
                             // splitting, is published so an idle lane of the block can trace it now
@@ -1839,11 +1840,11 @@ void rg_render_kernel(RgKernelArgs a) {
                         ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
                         unwind = true;
                     } else {
-                        Frame &f = stk[sp - 1];  // the FR_REFL_PEND pushed at the hit
+                        Frame &f = stk[sp++];  // rendering.rs:88
                         f.type = FR_REFL;
-                        f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b;
+                        f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = park[64 * PK_R];
                         // q = the reflection ray (origin = the shadow origin, direction set at the hit)
-                        qdepth = f.cdepth;
+                        qdepth = sp;  // the stack index is the depth (Frame::cdepth)
                         mode = MODE_CLOSEST;
                         n_sec++;
                     }
@@ -1911,8 +1912,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             Frame &f = stk[sp++];
                             f.type = FR_REFL;
                             f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = r;
-                            f.cdepth = cd;
-                            q = reflection(hn, hd, hp);
+                            q.o = add(hp, scl(hn, SHADOW_BIAS));  // ray.rs:57; q.d set at the hit
                             qdepth = cd;
                             mode = MODE_CLOSEST;
                             n_sec++;
@@ -1984,7 +1984,7 @@ void rg_render_kernel(RgKernelArgs a) {
                         f.type = FR_REFR_R;
                         q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
                         q.d = v3(f.rr[3], f.rr[4], f.rr[5]);
-                        qdepth = f.cdepth;
+                        qdepth = TASKS ? f.cdepth : sp;  // without tasks the stack index is the depth
                         mode = MODE_CLOSEST;
                         n_sec++;
                         break;
