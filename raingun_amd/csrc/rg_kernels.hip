@@ -1493,8 +1493,8 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // descriptors; LCOLD: bodies, materials), then every wave repeatedly takes the next 8x8 pixel
 // tile from an atomic queue (counters[16..], sharded) and runs the per-lane
 // state machine until its 64 lanes have written their pixels.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
-// Light path (LB > 1): blocks of RG_LIGHT_BLOCK_WAVES waves, at least WPS waves
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0>
+// TPW: light path, tiles per wave (0: RG_LIGHT_TILES_PER_WAVE).  Light path (LB > 1): blocks of RG_LIGHT_BLOCK_WAVES waves, at least WPS waves
 // per SIMD (the second bound is waves per execution unit on AMD); heavy path:
 // one block of 4*WPS waves per CU.  Both cap the VGPRs at 512 / WPS.
 __global__ __launch_bounds__(LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS, LB > 1 ? WPS : 1)
@@ -2040,7 +2040,8 @@ void rg_render_kernel(RgKernelArgs a) {
             if (tile == 0xFFFFFFFFu) {
                 tiles_left = false;
             } else {
-                constexpr uint32_t kmax = MAXD == 0 ? 0u : LB > 1 ? RG_LIGHT_TILES_PER_WAVE : RG_HEAVY_TILES_PER_WAVE;
+                constexpr uint32_t kmax = MAXD == 0 ? 0u : LB > 1 ? (TPW > 0 ? (uint32_t)TPW : RG_LIGHT_TILES_PER_WAVE)
+                                                                 : RG_HEAVY_TILES_PER_WAVE;
                 if constexpr (kmax > 0) {
                     // non-persistent: a wave renders at most kmax tiles, so the grid
                     // drains through the hardware dispatcher wave (block) by wave
@@ -2548,7 +2549,7 @@ static hipError_t occupancy(const void *kern, int threads, size_t lds, int &cus,
 
 // Launch (or, with grid_threads != nullptr, only size: the threads of the
 // grid, which a MAXD == 0 launch needs for its frame buffer) one instantiation.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0>
 static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream, size_t *grid_threads) {
     // Block size.  The heavy path shares one LDS copy of the scene (and the
     // BVH stacks / task pool) among the CU's 4*WPS waves: one block per CU.
@@ -2558,7 +2559,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     // waves that finished (a 4*WPS-wave block would keep the CU until its
     // slowest wave -- one refractive tile -- is done).
     constexpr int threads = LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS;  // LB > 1: the light path
-    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH, TASKS>;
+    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH, TASKS, TPW>;
     int cus = 0, per_cu = 0;
     const hipError_t oe = occupancy(reinterpret_cast<const void *>(kern), threads, lds, cus, per_cu);
     if (oe != hipSuccess) return oe;
@@ -2580,7 +2581,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
         if (cap < floor_blocks) cap = floor_blocks;
         if (blocks > cap) blocks = cap;
     }
-    constexpr unsigned long long kmax = MAXD == 0 ? 0 : LB > 1 ? RG_LIGHT_TILES_PER_WAVE : RG_HEAVY_TILES_PER_WAVE;
+    constexpr unsigned long long kmax = MAXD == 0 ? 0 : LB > 1 ? (TPW > 0 ? TPW : RG_LIGHT_TILES_PER_WAVE) : RG_HEAVY_TILES_PER_WAVE;
     if constexpr (kmax > 0)  // non-persistent: one wave per kmax tiles
         blocks = (tiles + waves * kmax - 1) / (waves * kmax);
     if (a->max_grid_threads && blocks * threads > a->max_grid_threads) blocks = a->max_grid_threads / threads;
@@ -2603,19 +2604,30 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
 #endif
 // RG_HEAVY_SCENE_BODIES and the path decision (rg_heavy_path) live in rg_device.h
 
-template <int MAXD, int WPS, int LB, bool F32F, bool BVH, bool TASKS>
+template <int MAXD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0>
 static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t *gt) {
     // the BVH kernels also hold the static per-wave traversal stacks
     constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u) -
                                 (uint32_t)(MAXD != 0 ? 0 : (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) * 64 * 4) -  // tile_px
                                 (TASKS ? (uint32_t)sizeof(TaskPool) : 0u);
     if (a->lds_total_bytes <= budget)  // whole scene (empty sphere part if n_sph == 0)
-        return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS>(a, a->lds_total_bytes, stream, gt);
+        return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_total_bytes, stream, gt);
     if (a->n_sph > 0 && a->lds_hot_bytes <= budget)
-        return launch_one<MAXD, true, false, WPS, LB, F32F, BVH, TASKS>(a, a->lds_hot_bytes, stream, gt);
-    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH, TASKS>(a, a->lds_lstack_bytes, stream, gt);
+        return launch_one<MAXD, true, false, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_hot_bytes, stream, gt);
+    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_lstack_bytes, stream, gt);
 }
 
+#ifndef RG_LIGHT_BIG_TPW
+// Light path, launches of at least RG_LIGHT_BIG_TILES tiles (4K frames and their halves): more
+// tiles per wave (fewer wave starts and scene stagings per frame: test1 0.2980 -> 0.2956 ms,
+// profiles/r03/late/ab_light_big_tpw.txt; 64 measures the same); smaller launches (the 1/4, 1/8
+// shares of a multi-GPU frame, host-visible bands) keep RG_LIGHT_TILES_PER_WAVE, which
+// measured faster for them.  0 = one tiles-per-wave for every launch.
+#define RG_LIGHT_BIG_TPW 32
+#endif
+#ifndef RG_LIGHT_BIG_TILES
+#define RG_LIGHT_BIG_TILES 50000ull  // whole 4K frames and 1/2 shares (test1 1/2 share 0.1504 -> 0.1490 ms)
+#endif
 #ifndef RG_LIGHT_WPS
 #define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
 #endif
@@ -2628,7 +2640,13 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
     // lane in ONE shared loop, 4 waves/SIMD to hide LDS/FP64 latency.
     const bool heavy = rg_heavy_path(*a);
 #ifndef RG_DEV_HEAVY_ONLY  // development builds: resource reports of the heavy kernels only
-    if (!heavy) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream, gt);
+    if (!heavy) {
+        if constexpr (MAXD != 0 && RG_LIGHT_BIG_TPW > 0) {
+            if (rg_tile_count(*a) >= RG_LIGHT_BIG_TILES)
+                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS, RG_LIGHT_BIG_TPW>(a, stream, gt);
+        }
+        return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream, gt);
+    }
 #endif
 #ifdef RG_DEV_LIGHT_ONLY  // development builds: resource reports of the light kernels only
     return hipErrorNotSupported;
