@@ -1049,7 +1049,9 @@ rg_status render_host_direct(const rg_scene *s, uint32_t W, uint32_t H, const rg
     hipStream_t rs = r.rs[0];
     void *dst = rg_host_device_ptr(rgba_out, std::max<size_t>(bytes, 1));
     const bool pageable = dst == nullptr;
-    const uint32_t wl = (uint32_t)s->host_tile_wlog, TH = 64u >> wl;
+    const bool light = !rg_heavy_path(rg_make_args(s));
+    const uint32_t wl = (uint32_t)(s->host_tile_forced || !light ? s->host_tile_wlog : RG_HOST_TILE_WLOG_LIGHT),
+                   TH = 64u >> wl;
     const size_t tiles_x = ((size_t)W + (1u << wl) - 1u) >> wl, tile_rows = (rows + TH - 1u) / TH,
                  ntiles = tiles_x * tile_rows;
     rg_status st = RG_OK;
@@ -1111,18 +1113,18 @@ rg_status rg_render_host(const rg_scene *s, uint32_t W, uint32_t H, const rg_til
     rg_status st = ensure_image_res(s);
     if (st != RG_OK) return st;
     rg_image_res &r = s->img;
-    // Path choice (profiles/r02/host_visible/hv_sweep.jsonl, 4K frames): one launch writing
-    // host memory wins for trace-dominated (heavy-path) scenes into page-locked
-    // buffers (synth1024: 2.99 vs 3.63 ms banded); for shading-dominated
-    // scenes the frame's PCIe writes stall the render waves (test1: 0.95 ms
-    // either way), and into pageable memory the per-tile publication costs
-    // more than the copies it overlaps (test1 2.5 vs 1.15 ms) -- banded there.
+    // Path choice (4K frames): into page-locked buffers one launch writing host
+    // memory wins -- heavy scenes (synth1024: 2.99 vs 3.63 ms banded,
+    // profiles/r02/host_visible/hv_sweep.jsonl) and, since the light path stores
+    // its tiles through an LDS ring in contiguous 4-KB runs of 64x1 tiles, light
+    // scenes too (test1 0.86 vs 0.93 ms, test3 0.82 vs 0.84:
+    // profiles/r03/late/hv_ring_group.txt); into pageable memory the per-tile
+    // publication costs more than the copies it overlaps (test1 2.5 vs 1.15
+    // ms) -- banded there.
     if (!rgb_out) {
         bool direct = s->image_bands < 0;
-        if (s->image_bands == 0) {
-            const RgKernelArgs pa = rg_make_args(s);
-            direct = rg_heavy_path(pa) && rg_host_device_ptr(rgba_out, std::max<size_t>((size_t)rows * W * 4, 1));
-        }
+        if (s->image_bands == 0)
+            direct = rg_host_device_ptr(rgba_out, std::max<size_t>((size_t)rows * W * 4, 1)) != nullptr;
         if (direct) return render_host_direct(s, W, H, t, rows, rgba_out, stats);
     }
 
@@ -1379,8 +1381,9 @@ rg_status rg_debug_set_image_bands(rg_scene *s, int32_t bands) {
 }
 
 rg_status rg_debug_set_host_tile_shape(rg_scene *s, int32_t tile_wlog) {
-    if (!s || tile_wlog < 3 || tile_wlog > 6) return RG_ERR_INVALID_ARGUMENT;
-    s->host_tile_wlog = tile_wlog;
+    if (!s || !(tile_wlog == 0 || (tile_wlog >= 3 && tile_wlog <= 6))) return RG_ERR_INVALID_ARGUMENT;
+    s->host_tile_wlog = tile_wlog == 0 ? RG_HOST_TILE_WLOG : tile_wlog;
+    s->host_tile_forced = tile_wlog != 0;
     return RG_OK;
 }
 

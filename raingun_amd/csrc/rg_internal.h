@@ -56,6 +56,11 @@ struct rg_launch_ctx {
 #define RG_IMAGE_STAGE_SLOTS 4  // pinned staging slots of the host-visible image path
 #define RG_IMAGE_MAX_BANDS 16   // events / counter snapshots per host-visible render or stream ring
 #define RG_IMAGE_BAND_PX (2u << 20)    // ~pixels per band of a banded host-visible frame
+#ifndef RG_HOST_TILE_WLOG_LIGHT
+// one-launch host-visible frames of light-path scenes: 64x1 tiles, so that a wave's ring of
+// consecutive tiles (rg_kernels.hip RG_HOST_RING) is one contiguous run of host memory
+#define RG_HOST_TILE_WLOG_LIGHT 6
+#endif
 #ifndef RG_HOST_TILE_WLOG
 #define RG_HOST_TILE_WLOG 3     // one-launch host-visible frames: 8x8 tiles (RgKernelArgs::tile_wlog)
 #endif
@@ -162,6 +167,7 @@ struct rg_scene {
     int tile_order = -1;  // expensive tiles first (rg_kernels.hip "tile ordering"): -1 auto (heavy path), 0, 1
     int image_bands = 0;  // host-visible frames: 0 auto, -1 one launch writing host memory, 1..16 row bands
     int host_tile_wlog = RG_HOST_TILE_WLOG;  // tile shape of the one-launch host-visible path
+    bool host_tile_forced = false;           // set by rg_debug_set_host_tile_shape (else light scenes: 64x1)
     // rg_render_multi (rg_debug_set_multi): 0 each device copies its rows to the host, 1 RCCL gather;
     // stand-in: every "device" is this one, gathers through a stand-in (tests on one GPU);
     // bands per device share in the direct mode (0: automatic)

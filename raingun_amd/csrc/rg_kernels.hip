@@ -1456,6 +1456,9 @@ __device__ __forceinline__ void pool_release(int slot) {  // owner: slot free ag
 
 using namespace rgk;
 
+#ifndef RG_HOST_RING
+#define RG_HOST_RING 16  // light path into pinned host memory: tiles per queue group and ring flush (0: one store per tile)
+#endif
 #ifndef RG_LIGHT_BLOCK_WAVES
 #define RG_LIGHT_BLOCK_WAVES 1  // light path: waves per block (blocks retire wave by wave)
 #endif
@@ -1599,6 +1602,18 @@ void rg_render_kernel(RgKernelArgs a) {
     constexpr bool HOSTF = MAXD == 0;
     __shared__ uint32_t tile_px[HOSTF ? (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) : 1][64];
     uint32_t *my_px = &tile_px[HOSTF ? threadIdx.x >> 6 : 0][lane];
+    // Light path into page-locked host memory without tile publication: the
+    // finished tiles of a wave collect in an LDS ring and go out RING at a time.
+    // A store to host memory completes only after its PCIe round trip, and on
+    // gfx9 every later `s_waitcnt vmcnt` (a texel load, a frame pop from the
+    // global frame buffer) waits for it too: one flush per RING tiles instead of
+    // one per tile.
+    constexpr int RING = (HOSTF && LB > 1) ? RG_HOST_RING : 0;
+    __shared__ uint32_t ring_px[RING > 0 ? RG_LIGHT_BLOCK_WAVES : 1][RING > 0 ? RING : 1][64];
+    __shared__ uint32_t ring_tile[RING > 0 ? RG_LIGHT_BLOCK_WAVES : 1][RING > 0 ? RING : 1];
+    [[maybe_unused]] const uint32_t rw = RING > 0 ? (threadIdx.x >> 6) % RG_LIGHT_BLOCK_WAVES : 0u;
+    [[maybe_unused]] uint32_t nring = 0;  // tiles waiting in the ring (wave-uniform)
+    [[maybe_unused]] uint32_t grp_next = 0, grp_end = 0;  // the wave's group of consecutive tiles (ring mode)
     // Light path: a diffuse hit's shading factors wait in LDS while its shadow
     // batch is traced (field k of the lane at park[k][lane], conflict-free), so
     // that only the query's own state is held in VGPRs across the trace.
@@ -1615,6 +1630,18 @@ void rg_render_kernel(RgKernelArgs a) {
     const uint32_t ntiles = tiles_x * ((a.out_rows + th - 1u) / th);
     const C3 def = c3(a.def[0], a.def[1], a.def[2]);
     const int max_depth = (int)a.max_depth;
+    [[maybe_unused]] const bool use_ring = RING > 0 && a.defer_px && !a.tile_flags;
+    // store the ring's tiles: each lane its pixel of every tile (same index rule as the tile start)
+    [[maybe_unused]] auto flush_ring = [&]() {
+        for (uint32_t k = 0; k < nring; ++k) {
+            const uint32_t tile = ring_tile[rw][k];
+            const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+            const uint32_t x = (tx << twlog) + ((uint32_t)lane & twmask);
+            const uint32_t orow = ty * th + ((uint32_t)lane >> twlog);
+            if (x < a.width && orow < a.out_rows) a.rgba[(size_t)orow * a.width + x] = ring_px[rw][k][lane];
+        }
+        nring = 0;
+    };
     uint32_t n_prim = 0, n_shadow = 0, n_sec = 0;
     FrameStack<MAXD> stk;
     stk.init(a);
@@ -2000,7 +2027,16 @@ void rg_render_kernel(RgKernelArgs a) {
         have_result = false;
         // every lane of the wave is done: its tile is complete (owners hold their pixels)
         if (HOSTF && my_tile != 0xFFFFFFFFu && (a.defer_px || a.tile_flags) && !__any(mode != MODE_DONE)) {
-            flush_tile(a, oidx, *my_px, my_tile, lane);
+            bool ringed = false;
+            if constexpr (RING > 0) {
+                if (use_ring) {
+                    ring_px[rw][nring][lane] = *my_px;
+                    if (lane == 0) ring_tile[rw][nring] = my_tile;
+                    if (++nring == (uint32_t)RING) flush_ring();
+                    ringed = true;
+                }
+            }
+            if (!ringed) flush_tile(a, oidx, *my_px, my_tile, lane);
             my_tile = 0xFFFFFFFFu;
         }
         // a wave with no live lane takes the next tile
@@ -2015,12 +2051,18 @@ void rg_render_kernel(RgKernelArgs a) {
             cur_tile = 0xFFFFFFFFu;
 #endif
             uint32_t tile = 0xFFFFFFFFu;
+            if constexpr (RING > 0) {  // the rest of the wave's group of consecutive tiles
+                if (use_ring && grp_next < grp_end) tile = grp_next++;
+            }
             if (HOSTF && a.cancel) {  // streaming: the consumer stopped (rendering.rs:53-67 `.all` short-circuits)
                 uint32_t cv = 0u;
                 if (lane == 0) cv = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (__builtin_amdgcn_readfirstlane(__shfl((int)cv, 0, 64)) != 0) qtried = RG_NQ;
             }
-            while (qtried < RG_NQ) {
+            // ring mode: the queue hands out groups of RING consecutive tiles (one contiguous
+            // run of host memory per ring flush: 4 KB with 64x1 tiles)
+            const uint32_t qlimit = (RING > 0 && use_ring) ? (ntiles + RING - 1) / RING : ntiles;
+            while (tile == 0xFFFFFFFFu && qtried < RG_NQ) {
                 uint32_t k = 0;
                 if (lane == 0) k = atomicAdd(reinterpret_cast<unsigned int *>(&a.counters[RG_QUEUE_BASE + RG_QUEUE_STRIDE * qi]), 1u);
                 k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
@@ -2028,10 +2070,21 @@ void rg_render_kernel(RgKernelArgs a) {
                 // head q serves tiles q, q+NQ, q+2NQ, ...: the tiles in flight stay a
                 // compact raster-order band of the frame, as with a single head
                 const unsigned long long t = (unsigned long long)k * RG_NQ + qi;
-                if (t < ntiles) { tile = (uint32_t)t; break; }
+                if (t < qlimit) {
+                    tile = (uint32_t)t;
+                    if constexpr (RING > 0) {
+                        if (use_ring) {
+                            tile = (uint32_t)t * RING;
+                            grp_next = tile + 1u;
+                            grp_end = min(tile + (uint32_t)RING, ntiles);
+                        }
+                    }
+                    break;
+                }
 #else
                 const uint32_t lo = (uint32_t)(((unsigned long long)ntiles * qi) / RG_NQ);
                 const uint32_t hi = (uint32_t)(((unsigned long long)ntiles * (qi + 1)) / RG_NQ);
+                static_assert(RG_HOST_RING == 0, "ring mode needs the interleaved queue");
                 if (lo + k < hi) { tile = lo + k; break; }
 #endif
                 qi = (qi + 1) % RG_NQ;
@@ -2289,7 +2342,21 @@ void rg_render_kernel(RgKernelArgs a) {
 #endif
         have_result = querying || mode == MODE_WAIT;
     }
-    if (HOSTF && my_tile != 0xFFFFFFFFu && (a.defer_px || a.tile_flags)) flush_tile(a, oidx, *my_px, my_tile, lane);
+    if (HOSTF && my_tile != 0xFFFFFFFFu && (a.defer_px || a.tile_flags)) {
+        bool ringed = false;
+        if constexpr (RING > 0) {
+            if (use_ring) {
+                ring_px[rw][nring][lane] = *my_px;
+                if (lane == 0) ring_tile[rw][nring] = my_tile;
+                ++nring;
+                ringed = true;
+            }
+        }
+        if (!ringed) flush_tile(a, oidx, *my_px, my_tile, lane);
+    }
+    if constexpr (RING > 0) {
+        if (use_ring) flush_ring();
+    }
 #ifdef RG_TILE_TIMES
     if (cur_tile != 0xFFFFFFFFu && lane == 0 && a.rgb) {
         a.rgb[cur_tile] = (float)(wall_clock64() - t_tile) * 0.01f;

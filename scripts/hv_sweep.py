@@ -36,7 +36,7 @@ def main():
             k, _, shape = setting.partition(":")
             k = int(k)
             _abi.check(lib.rg_debug_set_image_bands(ds.handle, k))
-            ds.set_host_tile_shape(int(shape or 3))
+            ds.set_host_tile_shape(int(shape or 0))  # no shape: the automatic one
             for _ in range(3):
                 ds.render_image(W, H, out=buf)
             n, t0 = 0, time.perf_counter()

@@ -63,7 +63,7 @@ def test_render_image_host_visible(oracle_lib, example_scenes, kind, w, h, bands
         ds.close()
 
 
-@pytest.mark.parametrize("wlog", [3, 4, 5, 6])
+@pytest.mark.parametrize("wlog", [0, 3, 4, 5, 6])  # 0: the automatic shape
 @pytest.mark.parametrize("kind,w,h", [("test1", 321, 243), ("synth200", 200, 111), ("test3", 97, 61)])
 def test_host_tile_shapes(oracle_lib, example_scenes, kind, w, h, wlog):
     """One-launch host-visible frames with every tile shape (8x8 .. 64x1; the
