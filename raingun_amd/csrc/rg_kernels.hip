@@ -1630,7 +1630,7 @@ void rg_render_kernel(RgKernelArgs a) {
     const uint32_t ntiles = tiles_x * ((a.out_rows + th - 1u) / th);
     const C3 def = c3(a.def[0], a.def[1], a.def[2]);
     const int max_depth = (int)a.max_depth;
-    [[maybe_unused]] const bool use_ring = RING > 0 && a.defer_px && !a.tile_flags;
+    [[maybe_unused]] const bool use_ring = RING > 0 && a.defer_px;
     // store the ring's tiles: each lane its pixel of every tile (same index rule as the tile start)
     [[maybe_unused]] auto flush_ring = [&]() {
         for (uint32_t k = 0; k < nring; ++k) {
@@ -1639,6 +1639,12 @@ void rg_render_kernel(RgKernelArgs a) {
             const uint32_t x = (tx << twlog) + ((uint32_t)lane & twmask);
             const uint32_t orow = ty * th + ((uint32_t)lane >> twlog);
             if (x < a.width && orow < a.out_rows) a.rgba[(size_t)orow * a.width + x] = ring_px[rw][k][lane];
+        }
+        if (a.tile_flags) {  // a consumer on the host: ONE system-scope release publishes the ring's tiles
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            if ((uint32_t)lane < nring)
+                __hip_atomic_store(&a.tile_flags[ring_tile[rw][lane]], a.frame_seq, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
         }
         nring = 0;
     };
