@@ -36,7 +36,10 @@ def main():
             k, _, shape = setting.partition(":")
             k = int(k)
             _abi.check(lib.rg_debug_set_image_bands(ds.handle, k))
-            ds.set_host_tile_shape(int(shape or 0))  # no shape: the automatic one
+            if shape:
+                ds.set_host_tile_shape(int(shape))
+            else:  # the automatic shape (libraries before round 3's tile ring reject 0: their default is 8x8)
+                lib.rg_debug_set_host_tile_shape(ds.handle, 0)
             for _ in range(3):
                 ds.render_image(W, H, out=buf)
             n, t0 = 0, time.perf_counter()
