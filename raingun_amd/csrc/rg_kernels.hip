@@ -1336,6 +1336,9 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 // flight too -- instead of 3072 persistent waves pinning their slots until the
 // frame's queue is empty.  0 = persistent.  16 measured best for the whole 4K
 // frame and for 1/2 .. 1/8 shares (profiles/r01/variants_light_tiles_per_wave.txt).
+#ifndef RG_PIPE_MIN_CU_DIV
+#define RG_PIPE_MIN_CU_DIV 3  // ... and at least 1/this of the CUs' blocks
+#endif
 #ifndef RG_PIPE_TILES_PER_WAVE
 #define RG_PIPE_TILES_PER_WAVE 32  // heavy launches with frames in flight (launch_one, RgKernelArgs::pipelined)
 #endif
@@ -2650,7 +2653,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
         // 0.713, 8K 1/8 1.250 -> 1.220; whole frames unchanged (profiles/r02/ab_pipe_blocks.txt)
         const unsigned long long per = waves * RG_PIPE_TILES_PER_WAVE;
         unsigned long long cap = (tiles + per - 1) / per;
-        const unsigned long long floor_blocks = ((unsigned long long)cus * per_cu + 2) / 3;
+        const unsigned long long floor_blocks = ((unsigned long long)cus * per_cu + RG_PIPE_MIN_CU_DIV - 1) / RG_PIPE_MIN_CU_DIV;
         if (cap < floor_blocks) cap = floor_blocks;
         if (blocks > cap) blocks = cap;
     }
