@@ -1337,7 +1337,7 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 // frame's queue is empty.  0 = persistent.  16 measured best for the whole 4K
 // frame and for 1/2 .. 1/8 shares (profiles/r01/variants_light_tiles_per_wave.txt).
 #ifndef RG_PIPE_MIN_CU_DIV
-#define RG_PIPE_MIN_CU_DIV 3  // ... and at least 1/this of the CUs' blocks
+#define RG_PIPE_MIN_CU_DIV 4  // ... and at least 1/this of the CUs' blocks (3 -> 4: north-star 1/8 share 0.349 -> 0.327 ms)
 #endif
 #ifndef RG_PIPE_TILES_PER_WAVE
 #define RG_PIPE_TILES_PER_WAVE 32  // heavy launches with frames in flight (launch_one, RgKernelArgs::pipelined)
@@ -2648,7 +2648,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     if (LB == 1 && MAXD != 0 && a->pipelined) {
         // Heavy path, frames in flight: each persistent block takes >= RG_PIPE_TILES_PER_WAVE
         // tiles per wave, so its lifetime dwarfs its start (LDS staging) and its slowest
-        // wave's tail, while every launch keeps >= 1/3 of the CUs; the other frames in
+        // wave's tail, while every launch keeps >= 1/RG_PIPE_MIN_CU_DIV of the CUs; the other frames in
         // flight fill the rest.  North-star 1/8 share 0.440 -> 0.399 ms, 1/4 0.753 ->
         // 0.713, 8K 1/8 1.250 -> 1.220; whole frames unchanged (profiles/r02/ab_pipe_blocks.txt)
         const unsigned long long per = waves * RG_PIPE_TILES_PER_WAVE;
