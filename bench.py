@@ -6,9 +6,17 @@ textures already resident in HBM, framebuffer left in HBM (rank 0 holds the
 assembled frame).  At N>1 (one rank per GPU: torchrun, or `--gpus N`, which
 launches torch.distributed.run itself) the frame is cut into 8-row tiles dealt
 round-robin to the ranks and the tiles are gathered to rank 0 with one RCCL
-gather per frame (ncclGather on the communicator of the torch.distributed
-"nccl" group, i.e. RCCL over xGMI), then re-interleaved into image order on
-rank 0 -- the per-frame loop runs in C++ (include/raingun_frames.h).
+gather per frame or two (ncclGather over xGMI on the library's own
+communicator: ncclCommInitRank, its unique id broadcast by torch.distributed),
+then re-interleaved into image order on rank 0 -- the per-frame loop runs in
+C++ (include/raingun_frames.h).  The line reports the ranks RCCL saw
+(`rccl_nranks`, `rccl.devices`).
+
+`value` is the device-resident kernel throughput: the frame is left in HBM
+(rank 0 holds the assembled frame).  SURVEY.md 8(d)'s scope -- "framebuffer
+available to host", as the reference's timer around render_image
+(src/render.rs:54-56) -- is the `host_visible` line (rg_render_image, the
+frame in host memory when each call returns).
 
 Workload (BASELINE.json configs[1]): examples/test1.yml at 3840x2160,
 recursion depth 5.  Extra line items on the same N GPUs: configs[2]
@@ -279,12 +287,20 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     pipe = None
     gather = world > 1 or args.rccl_rehearsal
     native = use_pipe and gather and args.backend == "nccl" and not args.python_pipeline
+    rccl = None
     if native:  # the per-frame loop in C++ (include/raingun_frames.h): render, ncclGather, re-interleave
-        try:
-            pipe = rd.NativeFramePipeline(ds, W, H, rank, world, TR, depth=F, device=dev)
-        except Exception as e:  # e.g. no communicator pointer from this torch build: same loop in Python
-            print(f"[bench] native frame pipeline unavailable ({e}); using the Python loop", file=sys.stderr)
-            native = False
+        # on the library's own RCCL communicator; a failure raises (the Python loop only on request)
+        pipe = rd.NativeFramePipeline(ds, W, H, rank, world, TR, depth=F, device=dev)
+        info = pipe.comm.info()
+        if info["nranks"] != world or info["rank"] != rank:
+            raise SystemExit(f"RCCL communicator {info} does not match rank {rank} of {world}")
+        infos = [None] * world
+        if world > 1:
+            dist.all_gather_object(infos, info)
+        else:
+            infos = [info]
+        rccl = {"nranks": info["nranks"], "devices": [i["device"] for i in infos],
+                "communicator": "ncclCommInitRank (rg_comm_init_rank; unique id broadcast by torch.distributed)"}
     if not native and use_pipe:
         pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TR, device=dev, depth=F,
                                 streams=F > 1 and not args.one_render_stream, gather=gather)
@@ -444,6 +460,9 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         # per single-stream launch: what the BVH and f32 pre-filter save, NOT a utilisation figure
         "reference_equivalent_fp64_tops": round(ref_equiv, 3),
     }
+    if rccl is not None:
+        res["rccl_nranks"] = rccl["nranks"]
+        res["rccl"] = rccl
     if bvh.enabled:
         res["bvh"] = {"nodes": bvh.nodes, "leaves": bvh.leaves, "depth": bvh.depth,
                       "box_margin": round(bvh.margin, 6), "near_origin_bound": round(bvh.origin_bound, 3)}

@@ -271,7 +271,9 @@ rg_status rg_trace(const rg_scene *scene, const double *rays, uint32_t n,
  * loaded).  No torch, no launcher: the drop-in for the reference's one
  * blocking call (rendering.rs:24-38, src/render.rs:55) on a whole node.
  * `stats` sums the devices' rays; on device errors error_pixel is the lowest
- * failing pixel of any device; kernel_ms spans the whole call. */
+ * failing pixel of any device; kernel_ms is device 0's render span (its
+ * launches, not the other devices' work or the copies to the host).  Every
+ * copy into rgba_out has landed when the call returns, on errors too. */
 rg_status rg_render_multi(const rg_scene *scene, uint32_t width, uint32_t height, int32_t ngpus,
                           uint32_t tile_rows, uint8_t *rgba_out, rg_stats *stats);
 

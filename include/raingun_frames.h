@@ -12,9 +12,10 @@
  * one-process Rayon loop of rendering::render_image (rendering.rs:24-38) for a
  * sequence of frames over a node.
  *
- * The RCCL communicator and ncclGather are the caller's (e.g. PyTorch's
- * ProcessGroupNCCL communicator and the librccl it loaded), passed as opaque
- * pointers, so the library links no collective library of its own.
+ * The communicator and the gather are passed as opaque pointers: normally
+ * the library's own (rg_comm_init_rank / rg_comm_gather_fn below: RCCL loaded
+ * at run time, so the library links no collective library), or any other
+ * ncclComm_t with its ncclGather.
  */
 #ifndef RAINGUN_FRAMES_H
 #define RAINGUN_FRAMES_H
@@ -58,7 +59,10 @@ rg_status rg_frames_step(rg_frames *frames);
  * so far, RG_OK if none; the frames are still delivered. */
 rg_status rg_frames_flush(rg_frames *frames);
 
-/* rg_frames_flush, plus the pixel of that first error (-1 if none). */
+/* Local status: waits for this rank's enqueued work and returns what
+ * rg_frames_flush would, plus the pixel of that first error (-1 if none).
+ * Never issues a collective: a batch still waiting for its gather stays
+ * pending (only rg_frames_flush, called on every rank, gathers it). */
 rg_status rg_frames_status(rg_frames *frames, int32_t *error_pixel);
 
 /* Rank 0: device pointer of the latest frame's assembled image (height rows of
@@ -66,9 +70,34 @@ rg_status rg_frames_status(rg_frames *frames, int32_t *error_pixel);
 const uint8_t *rg_frames_image(const rg_frames *frames);
 
 /* Rank 0: copy the latest assembled image to host memory (height*width*4
- * bytes); blocks until every enqueued frame is done.  Returns what
- * rg_frames_flush returns (the image is copied either way). */
+ * bytes).  Local: it issues no collective, so when a batch of frames is still
+ * waiting for its gather (batch 2, an odd number of steps since the last
+ * gather) it returns RG_ERR_INVALID_ARGUMENT -- call rg_frames_flush on EVERY
+ * rank first.  Otherwise it blocks until this rank's enqueued work is done and
+ * returns what rg_frames_flush returns (the image is copied either way). */
 rg_status rg_frames_read_image(const rg_frames *frames, uint8_t *host_out);
+
+/* ------------------------------------------------------------------------
+ * The library's own RCCL communicator for N processes (one per GPU), so a
+ * caller needs no collective library or torch internals of its own.  RCCL is
+ * loaded at run time (the librccl already in the process, else
+ * $RG_RCCL_LIBRARY, else librccl.so.1; RG_ERR_COLLECTIVE if none).
+ *   rank 0:     rg_comm_unique_id(id)              ncclGetUniqueId
+ *   caller:     hand the RG_COMM_ID_BYTES bytes of `id` to every rank
+ *   every rank: rg_comm_init_rank(id, world, rank, device, &comm)   ncclCommInitRank
+ *               (collective: all ranks call it; binds `device`)
+ *   rg_frames_create(..., comm, rg_comm_gather_fn(), ...)
+ *   rg_comm_destroy(comm) after rg_frames_destroy.
+ * ---------------------------------------------------------------------- */
+#define RG_COMM_ID_BYTES 128
+int32_t rg_comm_id_bytes(void);
+rg_status rg_comm_unique_id(uint8_t *id);
+rg_status rg_comm_init_rank(const uint8_t *id, int32_t world, int32_t rank, int32_t device, void **comm);
+/* ncclCommCount / ncclCommUserRank / ncclCommCuDevice of `comm` (each out pointer nullable). */
+rg_status rg_comm_info(void *comm, int32_t *nranks, int32_t *rank, int32_t *device);
+rg_status rg_comm_destroy(void *comm);
+/* ncclGather of the RCCL the communicators come from (NULL if RCCL cannot be loaded). */
+rg_gather_fn rg_comm_gather_fn(void);
 
 #ifdef __cplusplus
 }

@@ -142,7 +142,8 @@ DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "
                  "rg_debug_set_host_tile_shape", "rg_debug_set_multi", "rg_debug_gather_noop")
 # include/raingun_frames.h
 FRAMES_SYMBOLS = ("rg_frames_create", "rg_frames_destroy", "rg_frames_step", "rg_frames_flush", "rg_frames_image",
-                  "rg_frames_read_image", "rg_frames_status", "rg_frames_set_batch")
+                  "rg_frames_read_image", "rg_frames_status", "rg_frames_set_batch", "rg_comm_id_bytes",
+                  "rg_comm_unique_id", "rg_comm_init_rank", "rg_comm_info", "rg_comm_destroy", "rg_comm_gather_fn")
 PATH_AUTO, PATH_LIGHT, PATH_HEAVY = -1, 0, 1
 
 
@@ -238,6 +239,18 @@ def _declare(lib: C.CDLL) -> None:
     if hasattr(lib, "rg_frames_set_batch"):  # absent from pre-round-3 builds
         lib.rg_frames_set_batch.restype = C.c_int32
         lib.rg_frames_set_batch.argtypes = [C.c_void_p, C.c_int32]
+    if hasattr(lib, "rg_comm_init_rank"):  # absent from pre-round-4 builds
+        lib.rg_comm_id_bytes.restype = C.c_int32
+        lib.rg_comm_unique_id.restype = C.c_int32
+        lib.rg_comm_unique_id.argtypes = [C.c_void_p]
+        lib.rg_comm_init_rank.restype = C.c_int32
+        lib.rg_comm_init_rank.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, P(C.c_void_p)]
+        lib.rg_comm_info.restype = C.c_int32
+        lib.rg_comm_info.argtypes = [C.c_void_p, P(C.c_int32), P(C.c_int32), P(C.c_int32)]
+        lib.rg_comm_destroy.restype = C.c_int32
+        lib.rg_comm_destroy.argtypes = [C.c_void_p]
+        lib.rg_comm_gather_fn.restype = C.c_void_p
+        lib.rg_comm_gather_fn.argtypes = []
 
 
 def lib() -> C.CDLL:

@@ -214,7 +214,7 @@ rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t heigh
     // two frames per gather halve rank 0's per-frame enqueue cost (RCCL's host work
     // is per call); a depth that is not even keeps one
     f->batch = (world > 1 && depth % 2 == 0) ? 2 : 1;
-    const int B = 2;  // buffers sized for the largest batch (rg_frames_set_batch)
+    const int B = 2;  // batch buffers hold the largest batch (rg_frames_set_batch); batch p = slots 2p, 2p+1
     f->render.assign(depth, nullptr);
     for (int b = 0; b < depth && good; ++b) {
         stream(f->render[b]);
@@ -223,12 +223,12 @@ rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t heigh
         event(f->rendered);
         event(f->sent);
         event(f->done);
-        if (rank == 0) {
+        if (rank == 0) alloc(f->image, (size_t)height * width * 4);
+        if (b % B != 0) continue;  // one send / receive buffer per batch of B slots
+        if (rank == 0)
             alloc(f->gathered, f->slot_bytes * B * (size_t)world);
-            alloc(f->image, (size_t)height * width * 4);
-        } else {
+        else
             alloc(f->packed, f->slot_bytes * B);
-        }
     }
     stream(f->comm_stream);
     stream(f->side);
@@ -317,12 +317,11 @@ rg_status rg_frames_step(rg_frames *f) {
     return RG_OK;
 }
 
-rg_status rg_frames_flush(rg_frames *f) {
-    if (!f || !f->scene) return RG_ERR_INVALID_ARGUMENT;
-    if (f->pend_n > 0) {  // a batch cut short: gather what was rendered (every rank flushes at the same frame)
-        const rg_status st = issue_gather(f, f->pend_b0, f->pend_n);
-        if (st != RG_OK) return st;
-    }
+namespace {
+
+// Wait for this rank's enqueued work and collect its device errors -- local only:
+// never issues a collective (a gather that only one rank starts would hang).
+rg_status frames_sync_local(rg_frames *f) {
     for (hipStream_t s : f->render) {
         if (!ok(hipStreamSynchronize(s))) return RG_ERR_DEVICE;
         // device errors of this rank's renders (the reference panics: rendering.rs, bodies.rs:324, scene.rs:38)
@@ -338,9 +337,20 @@ rg_status rg_frames_flush(rg_frames *f) {
     return f->err;
 }
 
+}  // namespace
+
+rg_status rg_frames_flush(rg_frames *f) {
+    if (!f || !f->scene) return RG_ERR_INVALID_ARGUMENT;
+    if (f->pend_n > 0) {  // a batch cut short: gather what was rendered (every rank flushes at the same frame)
+        const rg_status st = issue_gather(f, f->pend_b0, f->pend_n);
+        if (st != RG_OK) return st;
+    }
+    return frames_sync_local(f);
+}
+
 rg_status rg_frames_status(rg_frames *f, int32_t *error_pixel) {
-    if (!f) return RG_ERR_INVALID_ARGUMENT;
-    const rg_status st = rg_frames_flush(f);
+    if (!f || !f->scene) return RG_ERR_INVALID_ARGUMENT;
+    const rg_status st = frames_sync_local(f);  // local: a pending batch stays pending (no collective here)
     if (error_pixel) *error_pixel = f->err_pixel;
     return st;
 }
@@ -351,10 +361,12 @@ const uint8_t *rg_frames_image(const rg_frames *f) {
 }
 
 rg_status rg_frames_read_image(const rg_frames *f, uint8_t *host_out) {
-    if (!f || !host_out || f->rank != 0) return RG_ERR_INVALID_ARGUMENT;
-    const rg_status st = rg_frames_flush(const_cast<rg_frames *>(f));  // gathers a batch cut short
-    if (st == RG_ERR_DEVICE || st == RG_ERR_INVALID_ARGUMENT) return st;
-    if (f->last < 0) return RG_ERR_INVALID_ARGUMENT;  // no frame yet
+    if (!f || !f->scene || !host_out || f->rank != 0) return RG_ERR_INVALID_ARGUMENT;
+    // a batch still waiting for its gather needs rg_frames_flush on EVERY rank first: the
+    // catch-up gather is a collective, which rank 0 must not start alone
+    if (f->pend_n > 0 || f->last < 0) return RG_ERR_INVALID_ARGUMENT;
+    const rg_status st = frames_sync_local(const_cast<rg_frames *>(f));
+    if (st == RG_ERR_DEVICE) return st;
     if (!ok(hipMemcpy(host_out, f->image[f->last], (size_t)f->h * f->w * 4, hipMemcpyDeviceToHost)))
         return RG_ERR_DEVICE;
     return st;  // the frame is delivered; a device error any frame raised is reported

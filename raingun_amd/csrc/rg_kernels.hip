@@ -1880,7 +1880,9 @@ void rg_render_kernel(RgKernelArgs a) {
                         f.type = FR_REFL;
                         f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = park[64 * PK_R];
                         // q = the reflection ray (origin = the shadow origin, direction set at the hit)
-                        qdepth = sp;  // the stack index is the depth (Frame::cdepth)
+                        // without task splitting the stack index is the depth; a lane tracing a pooled
+                        // subtree starts at sp = 0 with a non-zero depth, so TASKS keeps the hit's depth
+                        qdepth = TASKS ? qdepth + 1 : sp;
                         mode = MODE_CLOSEST;
                         n_sec++;
                     }

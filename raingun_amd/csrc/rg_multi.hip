@@ -42,6 +42,7 @@
 
 #include "../../include/raingun.h"
 #include "../../include/raingun_debug.h"
+#include "../../include/raingun_frames.h"
 #include "rg_internal.h"
 
 // rg_frames.hip: parts travel as packed RGB (3 B per pixel); device 0 reads its own part in place
@@ -60,6 +61,12 @@ typedef int (*pfn_comm_init_all)(void **comms, int ndev, const int *devlist);
 typedef int (*pfn_comm_destroy)(void *comm);
 typedef int (*pfn_gather)(const void *send, void *recv, size_t count, int dtype, int root, void *comm, hipStream_t s);
 typedef int (*pfn_group)(void);
+struct NcclUniqueId {  // ncclUniqueId (rccl.h): 128 opaque bytes, passed by value to ncclCommInitRank
+    char internal[RG_COMM_ID_BYTES];
+};
+typedef int (*pfn_get_unique_id)(NcclUniqueId *id);
+typedef int (*pfn_comm_init_rank)(void **comm, int nranks, NcclUniqueId id, int rank);
+typedef int (*pfn_comm_query)(void *comm, int *out);  // ncclCommCount / ncclCommCuDevice / ncclCommUserRank
 
 struct Rccl {
     bool tried = false;
@@ -68,6 +75,9 @@ struct Rccl {
     pfn_comm_destroy destroy = nullptr;
     pfn_gather gather = nullptr;
     pfn_group group_start = nullptr, group_end = nullptr;
+    pfn_get_unique_id get_unique_id = nullptr;
+    pfn_comm_init_rank init_rank = nullptr;
+    pfn_comm_query count = nullptr, cu_device = nullptr, user_rank = nullptr;
 };
 Rccl g_rccl;
 std::mutex g_rccl_mu;
@@ -99,7 +109,13 @@ const Rccl *rccl() {
         g_rccl.gather = reinterpret_cast<pfn_gather>(dlsym(h, "ncclGather"));
         g_rccl.group_start = reinterpret_cast<pfn_group>(dlsym(h, "ncclGroupStart"));
         g_rccl.group_end = reinterpret_cast<pfn_group>(dlsym(h, "ncclGroupEnd"));
-        if (g_rccl.init_all && g_rccl.destroy && g_rccl.gather && g_rccl.group_start && g_rccl.group_end) {
+        g_rccl.get_unique_id = reinterpret_cast<pfn_get_unique_id>(dlsym(h, "ncclGetUniqueId"));
+        g_rccl.init_rank = reinterpret_cast<pfn_comm_init_rank>(dlsym(h, "ncclCommInitRank"));
+        g_rccl.count = reinterpret_cast<pfn_comm_query>(dlsym(h, "ncclCommCount"));
+        g_rccl.cu_device = reinterpret_cast<pfn_comm_query>(dlsym(h, "ncclCommCuDevice"));
+        g_rccl.user_rank = reinterpret_cast<pfn_comm_query>(dlsym(h, "ncclCommUserRank"));
+        if (g_rccl.init_all && g_rccl.destroy && g_rccl.gather && g_rccl.group_start && g_rccl.group_end &&
+            g_rccl.get_unique_id && g_rccl.init_rank && g_rccl.count && g_rccl.cu_device && g_rccl.user_rank) {
             g_rccl.handle = h;
             return &g_rccl;
         }
@@ -217,6 +233,18 @@ void free_res(rg_multi_res *m) {
 }
 
 constexpr int kMaxBands = 4;
+
+// Wait for everything a call enqueued on any device (render, copy streams).  An
+// error exit from the band loop may leave earlier bands' copies into the
+// caller's buffer in flight: they must land before the call returns.
+void drain(rg_multi_res *m) {
+    for (int i = 0; i < (int)m->devs.size(); ++i) {
+        (void)hipSetDevice(m->devs[i]);
+        for (auto *v : {&m->streams, &m->streams2, &m->copies})
+            if (i < (int)v->size() && (*v)[i]) (void)hipStreamSynchronize((*v)[i]);
+    }
+    (void)hipGetLastError();
+}
 
 // Bands of a device's share (direct mode): K bands of J selected tiles each.
 int multi_bands(const rg_scene *s, uint32_t W, uint32_t H, int n) {
@@ -490,6 +518,7 @@ extern "C" rg_status rg_render_multi(const rg_scene *s, uint32_t W, uint32_t H, 
     }
     for (int i = 1; i < m->n; ++i) rg_sync_settings(m->reps[i], s);
     const rg_status st = m->mode == 1 ? render_gather(s, m, rgba_out, stats) : render_direct(s, m, rgba_out, stats);
+    if (st != RG_OK) drain(m);  // no copy into rgba_out may outlive the call
     (void)hipSetDevice(s->device);
     return st;
 }
@@ -504,3 +533,65 @@ extern "C" rg_status rg_debug_set_multi(rg_scene *s, int32_t mode, int32_t stand
     s->multi_only_rank = only_rank;
     return RG_OK;
 }
+
+// ---------------------------------------------------------------- communicators of N processes
+// (include/raingun_frames.h): the library's own RCCL communicator for the
+// one-process-per-GPU frame loop -- rank 0 makes the unique id, the caller
+// hands it to every rank (any channel: torch.distributed's store, MPI, a file),
+// and every rank joins with ncclCommInitRank on its device.  No torch internals.
+extern "C" {
+
+int32_t rg_comm_id_bytes(void) { return RG_COMM_ID_BYTES; }
+
+rg_status rg_comm_unique_id(uint8_t *id) {
+    if (!id) return RG_ERR_INVALID_ARGUMENT;
+    const Rccl *r = rccl();
+    if (!r) return RG_ERR_COLLECTIVE;
+    NcclUniqueId u;
+    if (r->get_unique_id(&u) != 0) return RG_ERR_COLLECTIVE;
+    std::memcpy(id, u.internal, sizeof u.internal);
+    return RG_OK;
+}
+
+rg_status rg_comm_init_rank(const uint8_t *id, int32_t world, int32_t rank, int32_t device, void **comm) {
+    if (!comm) return RG_ERR_INVALID_ARGUMENT;
+    *comm = nullptr;
+    if (!id || world < 1 || rank < 0 || rank >= world || device < 0) return RG_ERR_INVALID_ARGUMENT;
+    const Rccl *r = rccl();
+    if (!r) return RG_ERR_COLLECTIVE;
+    int ndev = 0;
+    if (!ok(hipGetDeviceCount(&ndev)) || device >= ndev) return RG_ERR_INVALID_ARGUMENT;
+    if (!ok(hipSetDevice(device))) return RG_ERR_DEVICE;  // ncclCommInitRank binds the current device
+    NcclUniqueId u;
+    std::memcpy(u.internal, id, sizeof u.internal);
+    void *c = nullptr;
+    if (r->init_rank(&c, world, u, rank) != 0 || !c) return RG_ERR_COLLECTIVE;
+    *comm = c;
+    return RG_OK;
+}
+
+rg_status rg_comm_info(void *comm, int32_t *nranks, int32_t *rank, int32_t *device) {
+    const Rccl *r = g_rccl.handle ? &g_rccl : nullptr;
+    if (!comm || !r) return RG_ERR_INVALID_ARGUMENT;
+    const std::pair<pfn_comm_query, int32_t *> q[3] = {{r->count, nranks}, {r->user_rank, rank}, {r->cu_device, device}};
+    for (const auto &e : q) {
+        int v = 0;
+        if (!e.second) continue;
+        if (e.first(comm, &v) != 0) return RG_ERR_COLLECTIVE;
+        *e.second = v;
+    }
+    return RG_OK;
+}
+
+rg_status rg_comm_destroy(void *comm) {
+    const Rccl *r = g_rccl.handle ? &g_rccl : nullptr;
+    if (!comm || !r) return RG_ERR_INVALID_ARGUMENT;
+    return r->destroy(comm) == 0 ? RG_OK : RG_ERR_COLLECTIVE;
+}
+
+rg_gather_fn rg_comm_gather_fn(void) {
+    const Rccl *r = rccl();
+    return r ? reinterpret_cast<rg_gather_fn>(r->gather) : nullptr;
+}
+
+}  // extern "C"

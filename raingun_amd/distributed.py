@@ -260,41 +260,68 @@ class FramePipeline:
                 torch.cuda.current_stream().wait_stream(s)
 
 
-def rccl_gather_fn() -> int:
-    """Address of ncclGather in the RCCL PyTorch loaded (the library behind its
-    "nccl" process group), for rg_frames_create."""
-    import ctypes as C
-    import os
+class RcclComm:
+    """The library's own RCCL communicator over the ranks of a torch.distributed
+    group (include/raingun_frames.h rg_comm_*): rank 0 makes the ncclUniqueId,
+    torch.distributed's public broadcast_object_list hands its bytes to every
+    rank, and every rank joins with ncclCommInitRank on `device` -- no private
+    torch API, no communicator borrowed from torch."""
 
-    import torch
+    def __init__(self, rank: int, world: int, device: int, group=None):
+        import ctypes as C
 
-    rccl = C.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))  # already loaded: same instance
-    return C.cast(rccl.ncclGather, C.c_void_p).value
+        import torch.distributed as dist
 
+        from . import _abi
 
-def rccl_comm_ptr(group=None, device=None) -> int:
-    """The ncclComm_t of a torch.distributed "nccl" process group (created by a
-    first collective if the group initialises lazily)."""
-    import torch
-    import torch.distributed as dist
+        self._lib = _abi.lib()
+        if not hasattr(self._lib, "rg_comm_init_rank"):
+            raise RuntimeError("libraingun_hip.so predates rg_comm_init_rank: rebuild it")
+        n = self._lib.rg_comm_id_bytes()
+        uid = (C.c_uint8 * n)()
+        if rank == 0:
+            _abi.check(self._lib.rg_comm_unique_id(uid), "rg_comm_unique_id")
+        obj = [bytes(uid)]
+        if world > 1:
+            dist.broadcast_object_list(obj, src=0, group=group)
+        uid = (C.c_uint8 * n).from_buffer_copy(obj[0])
+        h = C.c_void_p()
+        _abi.check(self._lib.rg_comm_init_rank(uid, world, rank, int(device), C.byref(h)), "rg_comm_init_rank")
+        self.handle = h
+        self.gather_fn = self._lib.rg_comm_gather_fn()
+        if not self.gather_fn:
+            raise RuntimeError("rg_comm_gather_fn: no ncclGather")
 
-    pg = group if group is not None else dist.distributed_c10d._get_default_group()
-    dist.all_reduce(torch.zeros(1, device=device), group=pg)
-    return pg._get_backend(torch.device("cuda", torch.cuda.current_device()))._comm_ptr()
+    def info(self) -> dict:
+        """ncclCommCount / ncclCommUserRank / ncclCommCuDevice of the communicator."""
+        import ctypes as C
+
+        from . import _abi
+
+        n, r, d = C.c_int32(-1), C.c_int32(-1), C.c_int32(-1)
+        _abi.check(self._lib.rg_comm_info(self.handle, C.byref(n), C.byref(r), C.byref(d)), "rg_comm_info")
+        return {"nranks": n.value, "rank": r.value, "device": d.value}
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.rg_comm_destroy(self.handle)
+            self.handle = None
 
 
 class NativeFramePipeline:
     """FramePipeline's N > 1 loop in C++ (include/raingun_frames.h): frame k
-    renders on render stream k % depth, ONE ncclGather per frame runs on a
-    communication stream in frame order, rank 0 re-interleaves on a side stream
-    -- a handful of HIP/RCCL calls per frame instead of ~70 us of Python on
-    rank 0, which would otherwise bound a small share (1/8 of a 4K test1 frame
-    renders in ~55 us).  Uses the communicator of the torch.distributed "nccl"
-    group and the RCCL library torch loaded."""
+    renders on render stream k % depth, ONE ncclGather per frame (or per two
+    frames) runs on a communication stream in frame order, rank 0
+    re-interleaves on a side stream -- a handful of HIP/RCCL calls per frame
+    instead of ~70 us of Python on rank 0, which would otherwise bound a small
+    share (1/8 of a 4K test1 frame renders in ~40 us).  The communicator is the
+    library's own (RcclComm, over the ranks of `group`); failures raise."""
 
     def __init__(self, scene, width: int, height: int, rank: int, world: int, tile_rows: int = TILE_ROWS,
                  depth: int = 4, group=None, device=None):
         import ctypes as C
+
+        import torch
 
         from . import _abi
 
@@ -304,10 +331,12 @@ class NativeFramePipeline:
         # must outlive its frames); a raw handle is the caller's to keep
         self._scene = scene
         scene_handle = getattr(scene, "handle", scene)
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.comm = RcclComm(rank, world, dev.index if dev.index is not None else torch.cuda.current_device(), group)
+        torch.cuda.set_device(dev)  # rg_frames_create binds the current device
         h = C.c_void_p()
         st = self._lib.rg_frames_create(scene_handle, width, height, tile_rows, rank, world, depth,
-                                        C.c_void_p(rccl_comm_ptr(group, device)), C.c_void_p(rccl_gather_fn()),
-                                        C.byref(h))
+                                        self.comm.handle, C.c_void_p(self.comm.gather_fn), C.byref(h))
         _abi.check(st, "rg_frames_create")
         self._h = h
 
@@ -322,7 +351,10 @@ class NativeFramePipeline:
         _abi.check(self._lib.rg_frames_flush(self._h), "rg_frames_flush")
 
     def read_frame(self):
-        """Rank 0: the latest assembled frame as a (H, W, 4) uint8 numpy array."""
+        """Rank 0: the latest assembled frame as a (H, W, 4) uint8 numpy array.
+        Local (no collective): call flush() on EVERY rank first -- with two
+        frames per gather, a batch cut short is gathered only by flush(), and
+        reading while it is pending raises (rg_frames_read_image)."""
         import numpy as np
 
         from . import _abi
@@ -335,6 +367,9 @@ class NativeFramePipeline:
         if getattr(self, "_h", None):
             self._lib.rg_frames_destroy(self._h)
             self._h = None
+        if getattr(self, "comm", None) is not None:
+            self.comm.close()  # after the frames: their gathers ran on it
+            self.comm = None
         self._scene = None
 
     def __del__(self):

@@ -124,9 +124,19 @@ def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, de
     if batch:  # 0: the default (two frames per gather at world > 1 with an even depth)
         _abi.check(lib.rg_frames_set_batch(hdl, batch))
     out = np.empty((h, w, 4), np.uint8)
+    b = batch or (2 if depth % 2 == 0 else 1)
     for k in range(2 * depth + 1):
         _abi.check(lib.rg_frames_step(hdl))
-        if k % 3 == 0:  # read_image flushes: batches cut short are gathered then
+        if k % 3 == 0:
+            if b == 2 and (k % depth) % 2 == 0:  # slot k % depth opens a batch of two
+                # a batch waits for its gather: reading (or asking for the status) must not
+                # start the catch-up gather, a collective, on rank 0 alone
+                n_calls = len(calls)
+                px = C.c_int32(-2)
+                assert lib.rg_frames_read_image(hdl, out.ctypes.data) == _abi.RG_ERR_INVALID_ARGUMENT, k
+                assert lib.rg_frames_status(hdl, C.byref(px)) == _abi.RG_OK and px.value == -1
+                assert len(calls) == n_calls, k
+            _abi.check(lib.rg_frames_flush(hdl))  # every rank flushes: a batch cut short is gathered then
             _abi.check(lib.rg_frames_read_image(hdl, out.ctypes.data))
             assert np.array_equal(out, ref), k
     _abi.check(lib.rg_frames_flush(hdl))
@@ -134,7 +144,6 @@ def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, de
     assert np.array_equal(out, ref)
     lib.rg_frames_destroy(hdl)
     ds.close()
-    b = batch or (2 if depth % 2 == 0 else 1)
     assert calls and all(c in (slot_bytes, b * slot_bytes) for c in calls)
     assert sum(calls) == (2 * depth + 1) * slot_bytes  # every frame gathered exactly once
     if b == 2:
