@@ -223,14 +223,14 @@ static tc_t texture_coords(const rg_body *b, v3 hit) {
 }
 
 /* ------------------------------------------------------------ material.rs */
-uint32_t rgo_wrap(float val, uint32_t max) { /* material.rs:129-138 */
+uint32_t rgo_wrap(float val, uint32_t max) { /* material.rs:70-79 */
     int32_t smax = (int32_t)max;
     float fc = val * (float)max;
     int32_t w = rgo_f32_to_i32(fc) % smax;
     return w < 0 ? (uint32_t)(w + smax) : (uint32_t)w;
 }
 
-static col material_color(const ctx_t *c, const rg_material *m, tc_t tc) { /* material.rs:115-148 */
+static col material_color(const ctx_t *c, const rg_material *m, tc_t tc) { /* material.rs:62-68, 82-89 */
     if (m->coloration == RG_COLORATION_COLOR) return col_make(m->color[0], m->color[1], m->color[2]);
     const rg_texture *t = &c->s->textures[m->texture];
     uint32_t x = rgo_wrap(tc.x + m->x_offset, t->width);

@@ -37,7 +37,7 @@ class SceneError(ValueError):
 
 # ---------------------------------------------------------------- data model
 @dataclass
-class Texture:                 # material.rs:85-91
+class Texture:                 # material.rs:26-32
     path: str
     image: np.ndarray          # (h, w, 4) uint8 RGBA
     x_offset: float
@@ -45,7 +45,7 @@ class Texture:                 # material.rs:85-91
 
 
 @dataclass
-class Material:                # material.rs:66-71
+class Material:                # material.rs:7-12
     coloration: Union[Color, Texture]
     albedo: float
     surface: str = "Diffuse"   # Diffuse | Reflecting | Refractive

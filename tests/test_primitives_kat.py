@@ -31,7 +31,7 @@ def test_fresnel_total_internal_reflection(oracle_lib):
     (3.0e9, 1500, 2147483647 % 1500),            # saturating `as i32`
     (-3.0e9, 1500, 1500 - (2147483648 % 1500)),  # i32::MIN % 1500 = -1148, +1500
 ])
-def test_wrap(oracle_lib, val, size, want):  # material.rs:129-138
+def test_wrap(oracle_lib, val, size, want):  # material.rs:70-79
     assert oracle_lib.lib().rgo_wrap(np.float32(val), size) == want
 
 

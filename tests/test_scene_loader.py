@@ -1,5 +1,5 @@
 """The YAML loader reproduces the serde schema of Scene (scene.rs:11-31,
-bodies.rs:13-47, lights.rs:8-26, material.rs:66-113)."""
+bodies.rs:13-47, lights.rs:8-26, material.rs:7-54)."""
 import numpy as np
 import pytest
 
