@@ -57,12 +57,12 @@ enum rg_body_kind {            /* bodies.rs:41-47 */
     RG_BODY_AABB = 3           /* p = {bounds[0].xyz, bounds[1].xyz}                          */
 };
 
-enum rg_coloration_kind {      /* material.rs:79-83 */
+enum rg_coloration_kind {      /* material.rs:20-24 */
     RG_COLORATION_COLOR = 0,
     RG_COLORATION_TEXTURE = 1
 };
 
-enum rg_surface_kind {         /* material.rs:108-113 */
+enum rg_surface_kind {         /* material.rs:49-54 */
     RG_SURFACE_DIFFUSE = 0,
     RG_SURFACE_REFLECTING = 1,
     RG_SURFACE_REFRACTIVE = 2
@@ -73,11 +73,11 @@ enum rg_light_kind {           /* lights.rs:22-26 */
     RG_LIGHT_SPHERICAL = 1     /* v = position  */
 };
 
-typedef struct rg_material {   /* material.rs:66-71 */
+typedef struct rg_material {   /* material.rs:7-12 */
     uint32_t coloration;       /* rg_coloration_kind */
     float color[3];            /* Coloration::Color, f32 RGB in [0,1] (color.rs:7-11) */
     int32_t texture;           /* Coloration::Texture: index into rg_scene_desc.textures */
-    float x_offset, y_offset;  /* Texture::{x_offset,y_offset} (material.rs:89-90) */
+    float x_offset, y_offset;  /* Texture::{x_offset,y_offset} (material.rs:30-31) */
     float albedo;
     uint32_t surface;          /* rg_surface_kind */
     float reflectivity;        /* Surface::Reflecting */

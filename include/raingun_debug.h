@@ -62,10 +62,12 @@ rg_status rg_debug_set_image_bands(rg_scene *scene, int32_t bands);
  * scenes, 64x1 for light-path scenes).  Device-resident renders always use 8x8. */
 rg_status rg_debug_set_host_tile_shape(rg_scene *scene, int32_t tile_wlog);
 
-/* rg_render_multi: mode 0 (default) = every device copies its rows of the
- * frame to the host buffer itself, over its own PCIe link, in `bands` row
- * bands per device (0 = automatic, 1..4) overlapped with the later bands'
- * renders; mode 1 = ONE RCCL ncclGather of the parts to the scene's device,
+/* rg_render_multi: mode 0 (default) = every device delivers its rows of the
+ * frame to the host buffer itself, over its own PCIe link: `bands` = -1 one
+ * launch per device whose kernel stores its rows straight into a page-locked
+ * frame, 1..4 row bands per device, each band's rows copied while the later
+ * bands render, 0 = automatic (one launch for heavy-path scenes into a
+ * page-locked frame, else bands); mode 1 = ONE RCCL ncclGather of the parts to the scene's device,
  * re-interleave there, one copy to the host.  stand_in = 1 places every
  * "device" on the scene's device (a replica each) and routes mode 1's gather
  * through a stand-in with ncclGather's signature and group semantics, so

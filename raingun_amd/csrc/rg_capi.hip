@@ -268,8 +268,9 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
                           uint8_t *rgba_dev, float *rgb_dev, hipStream_t st, unsigned long long *snap,
                           rg_launch_ctx **ctx_out, bool timed, uint32_t *tile_flags, uint32_t frame_seq,
                           const uint32_t *cancel, uint32_t tile_wlog, bool host_frame, bool pipelined,
-                          uint32_t tile_first, uint32_t tile_count) {
+                          uint32_t tile_first, uint32_t tile_count, bool image_rows) {
     if (tile_wlog < 3 || tile_wlog > 6) return RG_ERR_INVALID_ARGUMENT;
+    if (image_rows && (!host_frame || rgb_dev)) return RG_ERR_INVALID_ARGUMENT;
     if (!s || !rgba_dev || width == 0 || height == 0 || !tiling_valid(tiling)) return RG_ERR_INVALID_ARGUMENT;
     if (width < height) return RG_ERR_PORTRAIT;  // ray.rs:42
     const uint32_t sel_rows = rg_tiling_rows(height, tiling);  // every selected tile
@@ -304,6 +305,7 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     a.cancel = cancel;
     a.tile_wlog = tile_wlog;
     a.defer_px = host_frame ? 1u : 0u;
+    a.image_rows = image_rows ? 1u : 0u;
     a.pipelined = pipelined ? 1u : 0u;
     const int frames = frames_needed(s->max_depth);
     // host-frame launches run the MAXD == 0 kernels (the only ones with the

@@ -68,7 +68,7 @@ struct RgBodyDev {         // per body, YAML order
     double p[7];
 };
 
-struct RgMatDev {          // material.rs:66-71, flattened
+struct RgMatDev {          // material.rs:7-12 (+ Coloration 20-24, Surface 49-54), flattened
     int32_t coloration;
     float color[3];
     int32_t tex;
@@ -177,6 +177,10 @@ struct RgKernelArgs {
     // the 4 statistics words (rays by class, error key) there -- no copy after the kernel
     unsigned long long *snap_out;
     uint32_t max_grid_threads;  // nonzero: cap on the persistent grid (the deep frame buffer's memory bound)
+    // 1 (host-frame launches only): rgba is the WHOLE image and every pixel goes to its image row
+    // (y * width + x) instead of its dense output row -- a device of rg_render_multi writes its
+    // interleaved row tiles straight into the caller's frame (padding rows are not stored)
+    uint32_t image_rows;
     // nullable: the whole LDS arena [0, lds_total_bytes) as one device image (light path): a
     // block stages its scene copy with ONE unrolled loop instead of a loop per table
     const void *lds_blob;

@@ -208,7 +208,9 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
                           bool pipelined = false,    // frames in flight: size the grid for throughput
                           // a band of the tiling's selection: selected tiles [tile_first, tile_first + tile_count),
                           // rgba_dev / rgb_dev pointing at tile_first's first row
-                          uint32_t tile_first = 0, uint32_t tile_count = 0xFFFFFFFFu);
+                          uint32_t tile_first = 0, uint32_t tile_count = 0xFFFFFFFFu,
+                          // host_frame only: rgba_dev is the whole image, pixels go to their image rows
+                          bool image_rows = false);
 
 // Ray counts and status of a counter snapshot (stats nullable).
 rg_status rg_snap_status(const unsigned long long *snap, rg_stats *stats);

@@ -999,6 +999,9 @@ __device__ __forceinline__ bool ray_exotic(V3 o, V3 d) {
 // 8 + 3*8 FP64 ops per sphere instead of 3*16, with bit-identical per-ray
 // arithmetic.  Bit l of `occl` = light l of the batch is occluded.
 // RG_LB (lights per shadow batch on the light path) lives in rg_device.h
+#ifndef RG_LIGHT_SHADOW_FILTER
+#define RG_LIGHT_SHADOW_FILTER 0  // light path: f32 pre-filter in the shadow batches only
+#endif
 #ifndef RG_SHADOW_GROUP
 #define RG_SHADOW_GROUP 2  // spheres per miss-test group in the shadow pass
 #endif
@@ -1009,13 +1012,57 @@ struct ShadowBatch {
     double ld[LB];      // light.distance(hit) (lights.rs:53-58), +inf for directional
 };
 
-template <int LB, class Src>
+// F32F: the f32 pre-filter (above) in front of each group's exact tests: a group
+// runs the reference's f64 arithmetic only when some lane and light of the wave
+// may hit one of its spheres.  The batch's directions are unit vectors
+// (direction_from normalizes, lights.rs:46-51), so Kd is one constant (|d|^2 <=
+// 1.0001, checked per batch: a wave with another direction keeps the exact
+// tests only), and the threshold of a sphere is light-independent.
+template <int LB, bool F32F = false, class Src>
 __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &src, V3 o, const ShadowBatch<LB> &sb,
                                              uint32_t full, uint32_t &occl) {
     constexpr int G = RG_SHADOW_GROUP;
     const int n = a.n_sph, nfull = n - n % G;
+    [[maybe_unused]] constexpr float KD1 = 5.9604645e-08f * (16.2f + 26.2f * 1.0001f) * 1.01f;
+    [[maybe_unused]] bool filt = false;
+    [[maybe_unused]] float ox = 0.0f, oy = 0.0f, oz = 0.0f, kdo2 = 0.0f, fdx[LB], fdy[LB], fdz[LB];
+    if constexpr (F32F) {
+        bool unit = true;
+#pragma unroll
+        for (int l = 0; l < LB; ++l) {
+            unit &= dot(sb.d[l], sb.d[l]) <= 1.0001;  // NaN: false (exact tests only)
+            fdx[l] = (float)sb.d[l].x; fdy[l] = (float)sb.d[l].y; fdz[l] = (float)sb.d[l].z;
+        }
+        filt = !__any(!unit);
+        ox = (float)o.x; oy = (float)o.y; oz = (float)o.z;
+        kdo2 = KD1 * ((float)dot(o, o) * 1.000001f) * 1.000001f;  // >= Kd |o|^2 (make_rayf)
+    }
     for (int i = 0; i < n;) {
         const int g = i < nfull ? G : 1;  // wave-uniform
+        if constexpr (F32F) {
+            if (filt) {
+                bool cand = false;
+#pragma unroll
+                for (int k = 0; k < G; ++k) {
+                    if (k < g) {
+                        const RgSphF f = src.getf(i + k);
+                        const float hx = f.cx - ox, hy = f.cy - oy, hz = f.cz - oz;
+                        const float hh = __builtin_fmaf(hz, hz, __builtin_fmaf(hy, hy, hx * hx));
+                        const float thr = __builtin_fmaf(KD1, src.getf2(i + k).cchi, f.r2hi + kdo2);
+#pragma unroll
+                        for (int l = 0; l < LB; ++l) {
+                            const float adj = __builtin_fmaf(hz, fdz[l], __builtin_fmaf(hy, fdy[l], hx * fdx[l]));
+                            cand |= !(__builtin_fmaf(-adj, adj, hh) > thr) && !((occl >> l) & 1u);
+                        }
+                    }
+                }
+                if (!__any(cand)) {  // every lane and light of the wave certainly misses the group
+                    i += g;
+                    if ((i & 7) == 0 && !__any(occl != full)) return;
+                    continue;
+                }
+            }
+        }
         RgSph s[G];
         double hx[G], hy[G], hz[G], hh[G], adj[G][LB], opp[G][LB];
         bool cand[G][LB];
@@ -1146,13 +1193,13 @@ __device__ __forceinline__ void texture_coords(const RgBodyDev &b, V3 h, float &
     }
 }
 
-// material.rs:129-138
+// material.rs:70-79
 __device__ __forceinline__ uint32_t wrap(float v, int32_t max) {
     int32_t w = f32_to_i32(v * (float)max) % max;
     return w < 0 ? (uint32_t)(w + max) : (uint32_t)w;
 }
 
-// material.rs:115-148 + color.rs:26-30
+// material.rs:62-68, 82-89 + color.rs:26-30
 // (float)b / 255.0f for a byte b (material.rs Texture::color, color.rs from_rgba), correctly
 // rounded: one multiply and a residual correction instead of the IEEE division expansion.  Equal to
 // the division for every one of the 256 inputs (checked exhaustively: tests/test_primitives_kat.py).
@@ -1357,6 +1404,9 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+#ifndef RG_PRIO_DEPTH
+#define RG_PRIO_DEPTH 0    // > 0: waves with a query at this recursion depth or deeper run at raised priority
+#endif
 #ifndef RG_LIGHT_TASKS
 #define RG_LIGHT_TASKS 0   // task splitting on the light path (kernel template parameter TASKS)
 #endif
@@ -1374,57 +1424,82 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 #ifndef RG_TASK_SLOTS
 #define RG_TASK_SLOTS 128
 #endif
-struct TaskPool {
-    double ray[RG_TASK_SLOTS][6];  // published ray (origin, direction)
-    float col[RG_TASK_SLOTS][4];   // the subtree's colour once done
-    int depth[RG_TASK_SLOTS];      // recursion depth of the published ray
-    uint32_t pix[RG_TASK_SLOTS];   // owner's pixel (error reports)
-    int done[RG_TASK_SLOTS];       // 1: col holds the result
-    uint32_t free_m[RG_TASK_SLOTS / 32];  // 1 = slot free
-    uint32_t pend_m[RG_TASK_SLOTS / 32];  // 1 = published, not taken
-    int busy;                      // waves of the block that hold work
+#ifndef RG_LIGHT_TASK_SLOTS
+#define RG_LIGHT_TASK_SLOTS 32  // light path: the pool of a one-wave block (a few KB of LDS, not ~10)
+#endif
+template <int S>
+struct TaskPoolT {
+    static_assert(S % 32 == 0, "whole bitmap words");
+    double ray[S][6];  // published ray (origin, direction)
+    float col[S][4];   // the subtree's colour once done
+    int depth[S];      // recursion depth of the published ray
+    uint32_t pix[S];   // owner's pixel (error reports)
+    int done[S];       // 1: col holds the result
+    uint32_t free_m[S / 32];  // 1 = slot free
+    uint32_t pend_m[S / 32];  // 1 = published, not taken
+    int busy;                 // waves of the block that hold work
 };
-__shared__ TaskPool rg_pool;
+// one pool per block: the heavy path's (a CU's 12 waves) and the light path's
+// (a one-wave block); a kernel allocates only the one its instantiation uses
+__shared__ TaskPoolT<RG_TASK_SLOTS> rg_pool_h;
+__shared__ TaskPoolT<RG_LIGHT_TASK_SLOTS> rg_pool_l;
+template <bool L>
+__device__ __forceinline__ auto &pool_of() {
+    if constexpr (L) return rg_pool_l;
+    else return rg_pool_h;
+}
+template <bool L>
+constexpr int pool_slots() { return L ? RG_LIGHT_TASK_SLOTS : RG_TASK_SLOTS; }
 
 #define RG_WG __HIP_MEMORY_SCOPE_WORKGROUP
+template <bool L>
 __device__ __forceinline__ void pool_init() {
-    if (threadIdx.x < RG_TASK_SLOTS / 32) {
-        rg_pool.free_m[threadIdx.x] = ~0u;
-        rg_pool.pend_m[threadIdx.x] = 0u;
+    auto &P = pool_of<L>();
+    constexpr int S = pool_slots<L>();
+    if (threadIdx.x < S / 32) {
+        P.free_m[threadIdx.x] = ~0u;
+        P.pend_m[threadIdx.x] = 0u;
     }
-    if (threadIdx.x < RG_TASK_SLOTS) rg_pool.done[threadIdx.x] = 0;
-    if (threadIdx.x == 0) rg_pool.busy = 0;
+    for (uint32_t k = threadIdx.x; k < (uint32_t)S; k += blockDim.x) P.done[k] = 0;
+    if (threadIdx.x == 0) P.busy = 0;
 }
 // Claim a free slot (-1: pool full).  Lanes start at different words/bits.
+template <bool L>
 __device__ __forceinline__ int pool_alloc(int lane) {
+    auto &P = pool_of<L>();
+    constexpr int S = pool_slots<L>();
     const int rot = (lane >> 2) & 31;
-    for (int i = 0; i < RG_TASK_SLOTS / 32; ++i) {
-        const int w = (lane + i) & (RG_TASK_SLOTS / 32 - 1);
-        uint32_t m = __hip_atomic_load(&rg_pool.free_m[w], __ATOMIC_RELAXED, RG_WG);
+    for (int i = 0; i < S / 32; ++i) {
+        const int w = (lane + i) & (S / 32 - 1);
+        uint32_t m = __hip_atomic_load(&P.free_m[w], __ATOMIC_RELAXED, RG_WG);
         while (m != 0u) {
             const uint32_t r = rot ? ((m >> rot) | (m << (32 - rot))) : m;
             const int b = (__builtin_ctz(r) + rot) & 31;
             const uint32_t bit = 1u << b;
-            const uint32_t old = __hip_atomic_fetch_and(&rg_pool.free_m[w], ~bit, __ATOMIC_ACQUIRE, RG_WG);
+            const uint32_t old = __hip_atomic_fetch_and(&P.free_m[w], ~bit, __ATOMIC_ACQUIRE, RG_WG);
             if (old & bit) return w * 32 + b;
             m = old & ~bit;
         }
     }
     return -1;
 }
+template <bool L>
 __device__ __forceinline__ void pool_publish(int slot) {  // ray/depth/pix written before
-    __hip_atomic_fetch_or(&rg_pool.pend_m[slot >> 5], 1u << (slot & 31), __ATOMIC_RELEASE, RG_WG);
+    __hip_atomic_fetch_or(&pool_of<L>().pend_m[slot >> 5], 1u << (slot & 31), __ATOMIC_RELEASE, RG_WG);
 }
+template <bool L>
 __device__ __forceinline__ bool pool_any_pending() {
     uint32_t m = 0u;
 #pragma unroll
-    for (int w = 0; w < RG_TASK_SLOTS / 32; ++w) m |= __hip_atomic_load(&rg_pool.pend_m[w], __ATOMIC_RELAXED, RG_WG);
+    for (int w = 0; w < pool_slots<L>() / 32; ++w) m |= __hip_atomic_load(&pool_of<L>().pend_m[w], __ATOMIC_RELAXED, RG_WG);
     return m != 0u;
 }
 // Take the k-th pending task of a snapshot (k = rank among the wave's idle lanes).
+template <bool L>
 __device__ __forceinline__ int pool_take(int k) {
-    for (int w = 0; w < RG_TASK_SLOTS / 32; ++w) {
-        uint32_t m = __hip_atomic_load(&rg_pool.pend_m[w], __ATOMIC_RELAXED, RG_WG);
+    auto &P = pool_of<L>();
+    for (int w = 0; w < pool_slots<L>() / 32; ++w) {
+        uint32_t m = __hip_atomic_load(&P.pend_m[w], __ATOMIC_RELAXED, RG_WG);
         const int n = __builtin_popcount(m);
         if (k >= n) {
             k -= n;
@@ -1432,27 +1507,33 @@ __device__ __forceinline__ int pool_take(int k) {
         }
         for (int j = 0; j < k; ++j) m &= m - 1u;
         const uint32_t bit = m & (~m + 1u);
-        const uint32_t old = __hip_atomic_fetch_and(&rg_pool.pend_m[w], ~bit, __ATOMIC_ACQUIRE, RG_WG);
+        const uint32_t old = __hip_atomic_fetch_and(&P.pend_m[w], ~bit, __ATOMIC_ACQUIRE, RG_WG);
         return (old & bit) ? w * 32 + __builtin_ctz(bit) : -1;
     }
     return -1;
 }
+template <bool L>
 __device__ __forceinline__ bool pool_reclaim(int slot) {  // owner: un-publish if still pending
     const uint32_t bit = 1u << (slot & 31);
-    return (__hip_atomic_fetch_and(&rg_pool.pend_m[slot >> 5], ~bit, __ATOMIC_ACQ_REL, RG_WG) & bit) != 0u;
+    return (__hip_atomic_fetch_and(&pool_of<L>().pend_m[slot >> 5], ~bit, __ATOMIC_ACQ_REL, RG_WG) & bit) != 0u;
 }
+template <bool L>
 __device__ __forceinline__ void pool_finish(int slot, C3 c) {  // taker: result, then done
-    rg_pool.col[slot][0] = c.r;
-    rg_pool.col[slot][1] = c.g;
-    rg_pool.col[slot][2] = c.b;
-    __hip_atomic_store(&rg_pool.done[slot], 1, __ATOMIC_RELEASE, RG_WG);
+    auto &P = pool_of<L>();
+    P.col[slot][0] = c.r;
+    P.col[slot][1] = c.g;
+    P.col[slot][2] = c.b;
+    __hip_atomic_store(&P.done[slot], 1, __ATOMIC_RELEASE, RG_WG);
 }
+template <bool L>
 __device__ __forceinline__ bool pool_done(int slot) {
-    return __hip_atomic_load(&rg_pool.done[slot], __ATOMIC_ACQUIRE, RG_WG) != 0;
+    return __hip_atomic_load(&pool_of<L>().done[slot], __ATOMIC_ACQUIRE, RG_WG) != 0;
 }
+template <bool L>
 __device__ __forceinline__ void pool_release(int slot) {  // owner: slot free again
-    __hip_atomic_store(&rg_pool.done[slot], 0, __ATOMIC_RELAXED, RG_WG);
-    __hip_atomic_fetch_or(&rg_pool.free_m[slot >> 5], 1u << (slot & 31), __ATOMIC_RELEASE, RG_WG);
+    auto &P = pool_of<L>();
+    __hip_atomic_store(&P.done[slot], 0, __ATOMIC_RELAXED, RG_WG);
+    __hip_atomic_fetch_or(&P.free_m[slot >> 5], 1u << (slot & 31), __ATOMIC_RELEASE, RG_WG);
 }
 
 }  // namespace rgk
@@ -1500,12 +1581,14 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // tile from an atomic queue (counters[16..], sharded) and runs the per-lane
 // state machine until its 64 lanes have written their pixels.
 template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0>
-// TPW: light path, tiles per wave (0: RG_LIGHT_TILES_PER_WAVE).  Light path (LB > 1): blocks of RG_LIGHT_BLOCK_WAVES waves, at least WPS waves
+// TPW: light path, tiles per wave (0: RG_LIGHT_TILES_PER_WAVE; < 0: persistent waves that take tiles
+// until the queue is empty -- single launches, whose makespan is their slowest wave's tile sum).  Light path (LB > 1): blocks of RG_LIGHT_BLOCK_WAVES waves, at least WPS waves
 // per SIMD (the second bound is waves per execution unit on AMD); heavy path:
 // one block of 4*WPS waves per CU.  Both cap the VGPRs at 512 / WPS.
 __global__ __launch_bounds__(LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS, LB > 1 ? WPS : 1)
 void rg_render_kernel(RgKernelArgs a) {
     static_assert(!BVH || 4 * WPS <= RG_BVH_MAX_WAVES, "one BVH stack per wave");
+    constexpr bool PLIGHT = LB > 1;  // the light path's (smaller) task pool
     // the launch context's other counter set (the previous launch's, read back
     // already: same stream) starts the next launch at zero -- no memset per frame
     if (blockIdx.x == 0 && a.counters_next)
@@ -1587,7 +1670,7 @@ void rg_render_kernel(RgKernelArgs a) {
         T.texs = a.texs;
     }
     if (TASKS || LSPH || LCOLD) {
-        if constexpr (TASKS) pool_init();
+        if constexpr (TASKS) pool_init<PLIGHT>();
         __syncthreads();
     }
 
@@ -1641,7 +1724,10 @@ void rg_render_kernel(RgKernelArgs a) {
             const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
             const uint32_t x = (tx << twlog) + ((uint32_t)lane & twmask);
             const uint32_t orow = ty * th + ((uint32_t)lane >> twlog);
-            if (x < a.width && orow < a.out_rows) a.rgba[(size_t)orow * a.width + x] = ring_px[rw][k][lane];
+            if (x < a.width && orow < a.out_rows) {
+                const uint32_t row = a.image_rows ? out_row_to_y(a, orow) : orow;
+                if (row != 0xFFFFFFFFu) a.rgba[(size_t)row * a.width + x] = ring_px[rw][k][lane];
+            }
         }
         if (a.tile_flags) {  // a consumer on the host: ONE system-scope release publishes the ring's tiles
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -1693,7 +1779,7 @@ void rg_render_kernel(RgKernelArgs a) {
     bool tiles_left = true;    // the tile queue has not been found empty
     uint32_t my_tile = 0xFFFFFFFFu;  // the wave's current tile (published when done: a.tile_flags)
     [[maybe_unused]] uint32_t tiles_taken = 0;
-    [[maybe_unused]] bool counted = false;  // this wave is counted in rg_pool.busy
+    [[maybe_unused]] bool counted = false;  // this wave is counted in pool_of<PLIGHT>().busy
 #ifdef RG_TILE_TIMES
     uint32_t cur_tile = 0xFFFFFFFFu;  // diagnostic: per-tile time into rgb[tile] (us), wave iterations
     unsigned long long t_tile = 0, t_query = 0;  // into rgb[ntiles + tile], start, query time
@@ -1808,14 +1894,14 @@ void rg_render_kernel(RgKernelArgs a) {
                                     if (transmission(n, q.d, h, m.index, tr)) {
                                         trace_t = true;
                                         const Ray rr = reflection(n, q.d, h);
-                                        const int slot = pool_alloc(lane);
+                                        const int slot = pool_alloc<PLIGHT>(lane);
                                         if (slot >= 0) {
-                                            double *pr = rg_pool.ray[slot];
+                                            double *pr = pool_of<PLIGHT>().ray[slot];
                                             pr[0] = rr.o.x; pr[1] = rr.o.y; pr[2] = rr.o.z;
                                             pr[3] = rr.d.x; pr[4] = rr.d.y; pr[5] = rr.d.z;
-                                            rg_pool.depth[slot] = cd;
-                                            rg_pool.pix[slot] = pixel;
-                                            pool_publish(slot);
+                                            pool_of<PLIGHT>().depth[slot] = cd;
+                                            pool_of<PLIGHT>().pix[slot] = pixel;
+                                            pool_publish<PLIGHT>(slot);
                                             f.type = FR_REFR_TASK | (slot << 8);
                                         } else {
                                             f.type = FR_REFR_T;
@@ -1964,7 +2050,7 @@ void rg_render_kernel(RgKernelArgs a) {
                         bool handed = false;
                         if constexpr (TASKS) {
                             if (task >= 0) {  // a published subtree: hand its colour back
-                                pool_finish(task, ret);
+                                pool_finish<PLIGHT>(task, ret);
                                 task = -1;
                                 handed = true;
                             }
@@ -1988,11 +2074,11 @@ void rg_render_kernel(RgKernelArgs a) {
                             const int slot = f.type >> 8;
                             if (ftype == FR_REFR_TASK) {  // ret = the transmission subtree's colour
                                 f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
-                                if (pool_reclaim(slot)) {  // nobody took the reflection ray: trace it here
-                                    const double *r = rg_pool.ray[slot];
+                                if (pool_reclaim<PLIGHT>(slot)) {  // nobody took the reflection ray: trace it here
+                                    const double *r = pool_of<PLIGHT>().ray[slot];
                                     q.o = v3(r[0], r[1], r[2]);
                                     q.d = v3(r[3], r[4], r[5]);
-                                    pool_release(slot);
+                                    pool_release<PLIGHT>(slot);
                                     f.type = FR_REFR_R;
                                     qdepth = f.cdepth;
                                     mode = MODE_CLOSEST;
@@ -2001,12 +2087,12 @@ void rg_render_kernel(RgKernelArgs a) {
                                 }
                                 f.type = FR_REFR_WAIT | (slot << 8);
                             }
-                            if (!pool_done(slot)) {  // another lane is still tracing it
+                            if (!pool_done<PLIGHT>(slot)) {  // another lane is still tracing it
                                 mode = MODE_WAIT;
                                 break;
                             }
-                            const C3 rc = c3(rg_pool.col[slot][0], rg_pool.col[slot][1], rg_pool.col[slot][2]);
-                            pool_release(slot);
+                            const C3 rc = c3(pool_of<PLIGHT>().col[slot][0], pool_of<PLIGHT>().col[slot][1], pool_of<PLIGHT>().col[slot][2]);
+                            pool_release<PLIGHT>(slot);
                             const float kr = f.f[0];  // as FR_REFR_R below (rendering.rs:115-117)
                             C3 col = cadd(cscl(rc, kr), cscl(c3(f.f[5], f.f[6], f.f[7]), 1.0f - kr));
                             ret = cmul(cscl(col, f.f[1]), c3(f.f[2], f.f[3], f.f[4]));
@@ -2104,7 +2190,7 @@ void rg_render_kernel(RgKernelArgs a) {
             if (tile == 0xFFFFFFFFu) {
                 tiles_left = false;
             } else {
-                constexpr uint32_t kmax = MAXD == 0 ? 0u : LB > 1 ? (TPW > 0 ? (uint32_t)TPW : RG_LIGHT_TILES_PER_WAVE)
+                constexpr uint32_t kmax = MAXD == 0 || TPW < 0 ? 0u : LB > 1 ? (TPW > 0 ? (uint32_t)TPW : RG_LIGHT_TILES_PER_WAVE)
                                                                  : RG_HEAVY_TILES_PER_WAVE;
                 if constexpr (kmax > 0) {
                     // non-persistent: a wave renders at most kmax tiles, so the grid
@@ -2125,9 +2211,11 @@ void rg_render_kernel(RgKernelArgs a) {
                 bool alive = x < a.width && orow < a.out_rows;
                 const uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
                 oidx = (HOSTF && !alive) ? RG_NO_PIXEL : (size_t)orow * a.width + x;
+                if (HOSTF && a.image_rows && alive)  // the whole image: the pixel's own row (padding: no store)
+                    oidx = y == 0xFFFFFFFFu ? RG_NO_PIXEL : (size_t)y * a.width + x;
                 if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
                     if (HOSTF && a.defer_px) *my_px = 0u;
-                    else a.rgba[oidx] = 0u;
+                    else if (!HOSTF || oidx != RG_NO_PIXEL) a.rgba[oidx] = 0u;
 #ifndef RG_TILE_TIMES
                     if (a.rgb) { a.rgb[3 * oidx] = 0.0f; a.rgb[3 * oidx + 1] = 0.0f; a.rgb[3 * oidx + 2] = 0.0f; }
 #endif
@@ -2206,16 +2294,16 @@ void rg_render_kernel(RgKernelArgs a) {
             // idle lanes take subtrees other lanes of the block published
             const bool idle = mode == MODE_DONE;
             const unsigned long long want = __ballot(idle);
-            if (want != 0ull && pool_any_pending()) {
+            if (want != 0ull && pool_any_pending<PLIGHT>()) {
                 if (idle) {
-                    const int slot = pool_take((int)__builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
+                    const int slot = pool_take<PLIGHT>((int)__builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u)));
                     if (slot >= 0) {
-                        const double *r = rg_pool.ray[slot];
+                        const double *r = pool_of<PLIGHT>().ray[slot];
                         q.o = v3(r[0], r[1], r[2]);
                         q.d = v3(r[3], r[4], r[5]);
-                        qdepth = rg_pool.depth[slot];
-                        pixel = rg_pool.pix[slot];
+                        qdepth = pool_of<PLIGHT>().depth[slot];
+                        pixel = pool_of<PLIGHT>().pix[slot];
                         task = slot;
                         mode = MODE_CLOSEST;
                         n_sec++;  // the published reflection ray is traced here
@@ -2227,7 +2315,7 @@ void rg_render_kernel(RgKernelArgs a) {
         const bool wave_live = __any(live);
         if constexpr (TASKS) {
             if (wave_live != counted) {  // the block's count of waves holding work (helpers' exit test)
-                if (lane == 0) atomicAdd(&rg_pool.busy, wave_live ? 1 : -1);
+                if (lane == 0) atomicAdd(&pool_of<PLIGHT>().busy, wave_live ? 1 : -1);
                 counted = wave_live;
             }
         }
@@ -2235,7 +2323,7 @@ void rg_render_kernel(RgKernelArgs a) {
             if (tiles_left) continue;
             if constexpr (!TASKS) break;
             // tiles exhausted: serve the block's tasks until no wave holds work
-            if (!pool_any_pending() && __hip_atomic_load(&rg_pool.busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+            if (!pool_any_pending<PLIGHT>() && __hip_atomic_load(&pool_of<PLIGHT>().busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
                 break;
             __builtin_amdgcn_s_sleep(4);
             continue;
@@ -2274,6 +2362,15 @@ void rg_render_kernel(RgKernelArgs a) {
                     atomicAdd(&a.counters[15], (unsigned long long)__builtin_popcountll(all & ~shl));
                 }
             }
+        }
+#endif
+#if RG_PRIO_DEPTH > 0
+        // a wave deep in a ray tree (the slowest tiles' long chains, which bound a single launch's
+        // makespan) takes issue priority on its SIMD over waves on shallow work
+        {
+            const int myd = mode == MODE_CLOSEST ? qdepth : hdepth;
+            if (__any(querying && myd >= RG_PRIO_DEPTH)) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
         }
 #endif
 #ifdef RG_TILE_TIMES
@@ -2344,7 +2441,7 @@ void rg_render_kernel(RgKernelArgs a) {
             if (mode == MODE_SHADOW && !exact) {
                 occl = ~occl_full & ((1u << LB) - 1u);  // absent slots count as done
 #ifndef RG_DBG_NO_SHADOW_TRACE
-                trace_shadow<LB>(a, src, q.o, sb, (1u << LB) - 1u, occl);
+                trace_shadow<LB, F32F || RG_LIGHT_SHADOW_FILTER>(a, src, q.o, sb, (1u << LB) - 1u, occl);
 #endif
             }
         }
@@ -2659,7 +2756,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
         if (cap < floor_blocks) cap = floor_blocks;
         if (blocks > cap) blocks = cap;
     }
-    constexpr unsigned long long kmax = MAXD == 0 ? 0 : LB > 1 ? (TPW > 0 ? TPW : RG_LIGHT_TILES_PER_WAVE) : RG_HEAVY_TILES_PER_WAVE;
+    constexpr unsigned long long kmax = MAXD == 0 || TPW < 0 ? 0 : LB > 1 ? (TPW > 0 ? TPW : RG_LIGHT_TILES_PER_WAVE) : RG_HEAVY_TILES_PER_WAVE;
     if constexpr (kmax > 0)  // non-persistent: one wave per kmax tiles
         blocks = (tiles + waves * kmax - 1) / (waves * kmax);
     if (a->max_grid_threads && blocks * threads > a->max_grid_threads) blocks = a->max_grid_threads / threads;
@@ -2687,7 +2784,7 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
     // the BVH kernels also hold the static per-wave traversal stacks
     constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u) -
                                 (uint32_t)(MAXD != 0 ? 0 : (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) * 64 * 4) -  // tile_px
-                                (TASKS ? (uint32_t)sizeof(TaskPool) : 0u);
+                                (TASKS ? (uint32_t)(LB > 1 ? sizeof(TaskPoolT<RG_LIGHT_TASK_SLOTS>) : sizeof(TaskPoolT<RG_TASK_SLOTS>)) : 0u);
     if (a->lds_total_bytes <= budget)  // whole scene (empty sphere part if n_sph == 0)
         return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_total_bytes, stream, gt);
     if (a->n_sph > 0 && a->lds_hot_bytes <= budget)
@@ -2706,6 +2803,18 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 #ifndef RG_LIGHT_BIG_TILES
 #define RG_LIGHT_BIG_TILES 50000ull  // whole 4K frames and 1/2 shares (test1 1/2 share 0.1504 -> 0.1490 ms)
 #endif
+#ifndef RG_LIGHT_SINGLE_PERSISTENT
+#define RG_LIGHT_SINGLE_PERSISTENT 0  // light path: single launches run persistent waves (TPW < 0)
+#endif
+#ifndef RG_LIGHT_LATENCY_TASKS
+#define RG_LIGHT_LATENCY_TASKS 0  // light path: task splitting for single small launches (below RG_LIGHT_TASK_TILES)
+#endif
+#ifndef RG_LIGHT_TASK_TILES
+#define RG_LIGHT_TASK_TILES 50000ull
+#endif
+#ifndef RG_LIGHT_F32_FILTER
+#define RG_LIGHT_F32_FILTER false  // light path: f32 pre-filter in front of the exact sphere tests of closest-hit rays
+#endif
 #ifndef RG_LIGHT_WPS
 #define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
 #endif
@@ -2719,11 +2828,25 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
     const bool heavy = rg_heavy_path(*a);
 #ifndef RG_DEV_HEAVY_ONLY  // development builds: resource reports of the heavy kernels only
     if (!heavy) {
+        if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT) {
+            // a launch on its own (not one of several frames in flight): persistent waves at full
+            // occupancy balance the tiles dynamically, where a fixed tiles-per-wave grid makes every
+            // wave render exactly that many tiles and the slowest wave's sum the makespan
+            if (!a->pipelined)
+                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, RG_LIGHT_F32_FILTER, false, RG_LIGHT_TASKS, -1>(a, stream, gt);
+        }
+        if constexpr (MAXD != 0 && RG_LIGHT_LATENCY_TASKS && !RG_LIGHT_TASKS) {
+            // one small launch on its own (a single-shot share, rg_render_multi): its makespan is
+            // its slowest tiles' ray trees, so idle lanes of a wave take published subtrees
+            if (!a->pipelined && rg_tile_count(*a) < RG_LIGHT_TASK_TILES)
+                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, RG_LIGHT_F32_FILTER, false, true>(a, stream, gt);
+        }
         if constexpr (MAXD != 0 && RG_LIGHT_BIG_TPW > 0) {
             if (rg_tile_count(*a) >= RG_LIGHT_BIG_TILES)
-                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS, RG_LIGHT_BIG_TPW>(a, stream, gt);
+                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, RG_LIGHT_F32_FILTER, false, RG_LIGHT_TASKS,
+                                    RG_LIGHT_BIG_TPW>(a, stream, gt);
         }
-        return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, RG_LIGHT_TASKS>(a, stream, gt);
+        return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, RG_LIGHT_F32_FILTER, false, RG_LIGHT_TASKS>(a, stream, gt);
     }
 #endif
 #ifdef RG_DEV_LIGHT_ONLY  // development builds: resource reports of the light kernels only
@@ -2746,10 +2869,16 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
 // the global frame buffer (MAXD == 0).
 extern "C" int rg_max_array_frames(void) { return 64; }
 
+#ifndef RG_MAXD_SMALL
+#define RG_MAXD_SMALL 0  // > 0: also a frame array of this many frames (depth <= RG_MAXD_SMALL + 1 scenes)
+#endif
 static hipError_t dispatch_depth(const RgKernelArgs *a, int maxd, hipStream_t stream, size_t *gt) {
 #ifdef RG_DEV_ONE_DEPTH  // development builds: the MAXD = 8 instantiations only
     return maxd <= 8 ? launch_depth<8>(a, stream, gt) : hipErrorNotSupported;
 #else
+#if RG_MAXD_SMALL > 0
+    if (maxd <= RG_MAXD_SMALL) return launch_depth<RG_MAXD_SMALL>(a, stream, gt);
+#endif
     if (maxd <= 8) return launch_depth<8>(a, stream, gt);
     if (maxd <= 16) return launch_depth<16>(a, stream, gt);
     if (maxd <= 64) return launch_depth<64>(a, stream, gt);

@@ -397,6 +397,41 @@ rg_status render_gather(const rg_scene *s, rg_multi_res *m, uint8_t *rgba_out, r
     return merge_snaps(m, 1, stats);
 }
 
+// Direct path into a page-locked caller frame, one launch per device: every
+// device's kernel stores its finished tiles over its OWN PCIe link straight into
+// their image rows (RgKernelArgs::image_rows; the host-frame kernels' LDS tile
+// ring / per-tile stores, rg_kernels.hip), so the copy overlaps the render and
+// no band waits for a DMA -- a device's time is its render latency or its rows'
+// PCIe time, whichever is longer.
+rg_status render_direct_one(const rg_scene *s, rg_multi_res *m, uint8_t *dst, rg_stats *stats) {
+    const uint32_t W = m->w, H = m->h, T = m->T;
+    const int n = m->n;
+    const size_t frame_bytes = (size_t)H * W * 4;
+    const bool light = !rg_heavy_path(rg_make_args(s));
+    const uint32_t wl = (uint32_t)(s->host_tile_forced || !light ? s->host_tile_wlog : RG_HOST_TILE_WLOG_LIGHT);
+    if (!ok(hipSetDevice(m->devs[0])) || !ok(hipEventRecord(m->ev0, m->streams[0]))) return RG_ERR_DEVICE;
+    for (int i = 0; i < n; ++i) {
+        unsigned long long *snap = m->snap + 4 * i;
+        if (s->multi_only_rank >= 0 && i != s->multi_only_rank) {  // timeline rehearsal of one device
+            std::memset(snap, 0, 4 * sizeof(unsigned long long));
+            continue;
+        }
+        if (!ok(hipSetDevice(m->devs[i]))) return RG_ERR_DEVICE;
+        void *d = rg_host_device_ptr(dst, frame_bytes);  // registered portable: mapped on every device
+        if (!d) return RG_ERR_DEVICE;
+        const rg_tiling t = {T, (uint32_t)n, (uint32_t)i};
+        const rg_status st = rg_launch_tiles(m->reps[i], W, H, &t, static_cast<uint8_t *>(d), nullptr, m->streams[i],
+                                             snap, nullptr, false, nullptr, 0, nullptr, wl, true, false, 0,
+                                             0xFFFFFFFFu, true);
+        if (st != RG_OK) return st;
+    }
+    (void)hipSetDevice(m->devs[0]);
+    if (!ok(hipEventRecord(m->ev1, m->streams[0]))) return RG_ERR_DEVICE;
+    for (int i = n - 1; i >= 0; --i)
+        if (!ok(hipSetDevice(m->devs[i])) || !ok(hipStreamSynchronize(m->streams[i]))) return RG_ERR_DEVICE;
+    return merge_snaps(m, 1, stats);
+}
+
 // Direct path: every device renders its tiles in K bands and copies each band
 // straight to its image rows in page-locked host memory over its own link.
 rg_status render_direct(const rg_scene *s, rg_multi_res *m, uint8_t *rgba_out, rg_stats *stats) {
@@ -406,6 +441,12 @@ rg_status render_direct(const rg_scene *s, rg_multi_res *m, uint8_t *rgba_out, r
     // destination: the caller's buffer if page-locked, else the pinned frame
     uint8_t *dst = rg_host_is_pinned(rgba_out, frame_bytes) ? rgba_out : nullptr;
     const bool pageable = dst == nullptr;
+    // automatic (bands 0): trace-heavy scenes into a page-locked frame render in one launch per
+    // device (north star, one device's timeline 0.97 -> 0.87 ms); light scenes keep the bands,
+    // whose array kernels render a small share faster than the host-frame kernels (test1 0.27-0.31
+    // vs 0.49 ms: profiles/r04/latency_s1.json)
+    if (!pageable && (s->multi_bands < 0 || (s->multi_bands == 0 && rg_heavy_path(rg_make_args(s)))))
+        return render_direct_one(s, m, dst, stats);
     if (pageable) {
         if (!m->h_frame) {
             (void)hipSetDevice(m->devs[0]);
@@ -525,7 +566,7 @@ extern "C" rg_status rg_render_multi(const rg_scene *s, uint32_t W, uint32_t H, 
 
 extern "C" rg_status rg_debug_set_multi(rg_scene *s, int32_t mode, int32_t stand_in, int32_t bands,
                                         int32_t only_rank) {
-    if (!s || mode < 0 || mode > 1 || bands < 0 || bands > kMaxBands || only_rank < -1) return RG_ERR_INVALID_ARGUMENT;
+    if (!s || mode < 0 || mode > 1 || bands < -1 || bands > kMaxBands || only_rank < -1) return RG_ERR_INVALID_ARGUMENT;
     if (only_rank >= 0 && (mode != 0 || !stand_in)) return RG_ERR_INVALID_ARGUMENT;
     s->multi_mode = mode;
     s->multi_stand_in = stand_in != 0;

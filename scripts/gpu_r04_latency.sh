@@ -13,6 +13,8 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 "$O/pytest.log"
 timeout -k 10 240 python scripts/latency_probe.py test1 synth1024 > "$O/base.json" 2> "$O/base.err" || { tail "$O/base.err"; exit 1; }
 echo base; cat "$O/base.json"
+timeout -k 10 240 python scripts/latency_probe.py --tile-order test1 > "$O/base_order.json" 2> "$O/base_order.err" || { tail "$O/base_order.err"; exit 1; }
+echo base_order; cat "$O/base_order.json"
 for v in "$@"; do
   case $v in
     tt*) RAINGUN_HIP_LIB=$R/abvar/$v/libraingun_hip.so timeout -k 10 240 python scripts/tail_probe.py timeline > "$O/$v.json" 2> "$O/$v.err" || { tail "$O/$v.err"; exit 1; } ;;
