@@ -41,6 +41,7 @@
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream);
 extern "C" hipError_t rg_render_grid_threads(const RgKernelArgs *a, int maxd, size_t *threads);
 extern "C" int rg_max_array_frames(void);
+extern "C" int rg_launch_global_frames(const RgKernelArgs *a, int maxd);
 extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scratch, uint32_t *perm, hipStream_t stream);
 extern "C" size_t rg_tile_order_scratch_words(uint32_t ntiles);
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,
@@ -312,7 +313,7 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     // host-frame features: rg_kernels.hip HOSTF), whose frames live in a
     // global buffer like those of recursion deeper than the compiled arrays
     const int disp = host_frame ? std::max(frames, rg_max_array_frames() + 1) : frames;
-    if (disp > rg_max_array_frames() && out_rows > 0) {
+    if (rg_launch_global_frames(&a, disp) && out_rows > 0) {
         // frames in a global buffer sized for this launch's (persistent) grid
         size_t threads = 0;
         if (!ok(rg_render_grid_threads(&a, disp, &threads)) || threads == 0 || threads > 0xFFFFFFFFull)

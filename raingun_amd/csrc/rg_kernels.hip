@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <mutex>
 #include <type_traits>
 #include <utility>
@@ -1327,15 +1328,67 @@ struct FrameStack {
     __device__ __forceinline__ void init(const RgKernelArgs &) {}
     __device__ __forceinline__ Frame &operator[](int i) { return f[i]; }
 };
+// Global frames are stored field-major, like scratch: dword k of frame i of grid
+// thread g at plane (i * RG_FRAME_DWORDS + k), element g, so each field access
+// of a wave is one coalesced 256-B run (a Frame-struct array would make every
+// field a 64-line gather at an 88-B stride).  FrameRefG mirrors Frame's fields.
+constexpr int RG_FRAME_DWORDS = (int)(sizeof(Frame) / 4);
+static_assert(offsetof(Frame, f) == 0 && offsetof(Frame, rr) == 32 && offsetof(Frame, type) == 80 &&
+                  offsetof(Frame, cdepth) == 84 && RG_FRAME_DWORDS == 22,
+              "FrameRefG plane numbers");
+struct FrameRefG {
+    uint32_t *p;      // plane 0 of this frame, this thread
+    uint32_t stride;  // dwords between planes (grid threads)
+    struct F {        // a float field
+        uint32_t *q;
+        __device__ __forceinline__ void operator=(float v) const { *q = __float_as_uint(v); }
+        __device__ __forceinline__ operator float() const { return __uint_as_float(*q); }
+    };
+    struct D {        // a double field: two planes
+        uint32_t *q;
+        uint32_t stride;
+        __device__ __forceinline__ void operator=(double v) const {
+            const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+            q[0] = (uint32_t)b;
+            q[stride] = (uint32_t)(b >> 32);
+        }
+        __device__ __forceinline__ operator double() const {
+            return __longlong_as_double((long long)(((unsigned long long)q[stride] << 32) | q[0]));
+        }
+    };
+    struct I {        // an int field
+        uint32_t *q;
+        __device__ __forceinline__ void operator=(int v) const { *q = (uint32_t)v; }
+        __device__ __forceinline__ operator int() const { return (int)*q; }
+    };
+    struct FA {
+        uint32_t *q;
+        uint32_t stride;
+        __device__ __forceinline__ F operator[](int k) const { return F{q + (size_t)k * stride}; }
+    };
+    struct DA {
+        uint32_t *q;
+        uint32_t stride;
+        __device__ __forceinline__ D operator[](int k) const { return D{q + (size_t)(2 * k) * stride, stride}; }
+    };
+    FA f;
+    DA rr;
+    I type, cdepth;
+    __device__ __forceinline__ FrameRefG(uint32_t *p0, uint32_t s)
+        : p(p0), stride(s), f{p0, s}, rr{p0 + (size_t)8 * s, s}, type{p0 + (size_t)20 * s},
+          cdepth{p0 + (size_t)21 * s} {}
+};
 template <>
 struct FrameStack<0> {
-    Frame *base;
-    uint32_t stride;
+    uint32_t *base;   // plane 0 of frame 0, this thread
+    uint32_t stride;  // grid threads
     __device__ __forceinline__ void init(const RgKernelArgs &a) {
         stride = a.deep_stride;
-        base = static_cast<Frame *>(a.deep_stack) + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+        base = static_cast<uint32_t *>(a.deep_stack) + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     }
-    __device__ __forceinline__ Frame &operator[](int i) { return base[(size_t)i * stride]; }
+    __device__ __forceinline__ FrameRefG operator[](int i) {
+        return FrameRefG(base + (size_t)i * RG_FRAME_DWORDS * stride, stride);
+    }
 };
 
 
@@ -1404,6 +1457,9 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+#ifndef RG_LIGHT_GLOBAL_FRAMES
+#define RG_LIGHT_GLOBAL_FRAMES 0  // light path: shading frames field-major in global memory instead of a scratch array
+#endif
 #ifndef RG_PRIO_DEPTH
 #define RG_PRIO_DEPTH 0    // > 0: waves with a query at this recursion depth or deeper run at raised priority
 #endif
@@ -1589,6 +1645,7 @@ __global__ __launch_bounds__(LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS, LB 
 void rg_render_kernel(RgKernelArgs a) {
     static_assert(!BVH || 4 * WPS <= RG_BVH_MAX_WAVES, "one BVH stack per wave");
     constexpr bool PLIGHT = LB > 1;  // the light path's (smaller) task pool
+    constexpr bool GFRAMES = MAXD == 0 || (LB > 1 && RG_LIGHT_GLOBAL_FRAMES);
     // the launch context's other counter set (the previous launch's, read back
     // already: same stream) starts the next launch at zero -- no memset per frame
     if (blockIdx.x == 0 && a.counters_next)
@@ -1738,7 +1795,7 @@ void rg_render_kernel(RgKernelArgs a) {
         nring = 0;
     };
     uint32_t n_prim = 0, n_shadow = 0, n_sec = 0;
-    FrameStack<MAXD> stk;
+    FrameStack<GFRAMES ? 0 : MAXD> stk;  // GFRAMES: field-major frames in a global buffer, no scratch array
     stk.init(a);
 
     // Sharded tile queue: RG_NQ heads, each owning a contiguous band of tiles
@@ -1880,7 +1937,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             ret = cmul(cscl(col, m.transparency), surf);
                             unwind = true;
                         } else {
-                            Frame &f = stk[sp++];
+                            auto &&f = stk[sp++];
                             f.f[0] = kr; f.f[1] = m.transparency;
                             f.f[2] = surf.r; f.f[3] = surf.g; f.f[4] = surf.b;
                             if constexpr (TASKS) f.cdepth = cd;
@@ -1962,7 +2019,7 @@ void rg_render_kernel(RgKernelArgs a) {
                         ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
                         unwind = true;
                     } else {
-                        Frame &f = stk[sp++];  // rendering.rs:88
+                        auto &&f = stk[sp++];  // rendering.rs:88
                         f.type = FR_REFL;
                         f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = park[64 * PK_R];
                         // q = the reflection ray (origin = the shadow origin, direction set at the hit)
@@ -2033,7 +2090,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
                             unwind = true;
                         } else {
-                            Frame &f = stk[sp++];
+                            auto &&f = stk[sp++];
                             f.type = FR_REFL;
                             f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = r;
                             q.o = add(hp, scl(hn, SHADOW_BIAS));  // ray.rs:57; q.d set at the hit
@@ -2067,7 +2124,7 @@ void rg_render_kernel(RgKernelArgs a) {
                         mode = MODE_DONE;
                         break;
                     }
-                    Frame &f = stk[sp - 1];
+                    auto &&f = stk[sp - 1];
                     if constexpr (TASKS) {
                         const int ftype = f.type & 0xFF;
                         if (ftype == FR_REFR_TASK || ftype == FR_REFR_WAIT) {
@@ -2765,7 +2822,8 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
         *grid_threads = (size_t)blocks * threads;
         return hipSuccess;
     }
-    if (MAXD == 0 && (a->deep_stack == nullptr || (unsigned long long)a->deep_stride < blocks * threads))
+    constexpr bool GFRAMES = MAXD == 0 || (LB > 1 && RG_LIGHT_GLOBAL_FRAMES);
+    if (GFRAMES && (a->deep_stack == nullptr || (unsigned long long)a->deep_stride < blocks * threads))
         return hipErrorInvalidValue;  // the caller sized the frame buffer for another grid
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), lds, stream, *a);
     return hipGetLastError();
@@ -2868,6 +2926,13 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
 // Frame-stack capacity of each compiled array instantiation; deeper scenes use
 // the global frame buffer (MAXD == 0).
 extern "C" int rg_max_array_frames(void) { return 64; }
+
+// Does this launch keep its frames in the launch context's global buffer (the
+// host sizes it with rg_render_grid_threads)?  Depths above the arrays always;
+// light launches too when built with RG_LIGHT_GLOBAL_FRAMES (no scratch array).
+extern "C" int rg_launch_global_frames(const RgKernelArgs *a, int maxd) {
+    return maxd > rg_max_array_frames() || (RG_LIGHT_GLOBAL_FRAMES && !rg_heavy_path(*a));
+}
 
 #ifndef RG_MAXD_SMALL
 #define RG_MAXD_SMALL 0  // > 0: also a frame array of this many frames (depth <= RG_MAXD_SMALL + 1 scenes)

@@ -81,10 +81,33 @@ def main():
                 launch(i, streams[i % 8], True)
             torch.cuda.synchronize()
             pipe_ms = (time.perf_counter() - t0) * 1e3 / (8 * K)
-            for s in streams:
-                ds.release_stream(s.cuda_stream)
             r[name] = {"sync_ms": round(sync_ms, 4), "b2b_ms": round(b2b_ms, 4), "spaced_ms": round(spaced_ms, 4),
                        "pipelined_8_streams_ms": round(pipe_ms, 4)}
+            # the same tiles as ONE call split into k concurrent launches on k streams (tile j of the
+            # call's selection -> launch j % k), from a start event to the join of all k
+            for k in (2, 4, 8):
+                subs = [_abi.rg_tiling(8, stride * k, j * stride) for j in range(k)]
+                sbufs = [torch.empty((lib.rg_tiling_rows(H, C.byref(u)), W, 4), dtype=torch.uint8, device="cuda")
+                         for u in subs]
+                ss = streams[:k]
+                ts = []
+                for rep in range(K + 3):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(s0)
+                    for j in range(k):
+                        ss[j].wait_event(e0)
+                        _abi.check(lib.rg_render_tiles_async(ds.handle, W, H, C.byref(subs[j]),
+                                                             C.c_void_p(sbufs[j].data_ptr()), None,
+                                                             C.c_void_p(ss[j].cuda_stream), None))
+                    for j in range(k):
+                        s0.wait_stream(ss[j])
+                    e1.record(s0)
+                    torch.cuda.synchronize()
+                    if rep >= 3:
+                        ts.append(e0.elapsed_time(e1))
+                r[name][f"split{k}_ms"] = round(sorted(ts)[len(ts) // 2], 4)
+            for st_ in streams:
+                ds.release_stream(st_.cuda_stream)
             print(wl, name, r[name], file=sys.stderr, flush=True)
         ds.close()
         out[wl] = r
