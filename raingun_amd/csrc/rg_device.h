@@ -181,6 +181,10 @@ struct RgKernelArgs {
     // (y * width + x) instead of its dense output row -- a device of rg_render_multi writes its
     // interleaved row tiles straight into the caller's frame (padding rows are not stored)
     uint32_t image_rows;
+    // > 1: this launch is part j = out_tile_add of a call split into out_tile_mul launches (the
+    // call's selected tile i -> launch i % mul); its selected tile s is written as the call's
+    // tile s * mul + add, so the parts together fill the call's dense output
+    uint32_t out_tile_mul, out_tile_add;
     // nullable: the whole LDS arena [0, lds_total_bytes) as one device image (light path): a
     // block stages its scene copy with ONE unrolled loop instead of a loop per table
     const void *lds_blob;

@@ -1398,6 +1398,15 @@ __device__ __forceinline__ uint32_t out_row_to_y(const RgKernelArgs &a, uint32_t
     return y >= a.height ? 0xFFFFFFFFu : (uint32_t)y;
 }
 
+// Output row of the launch's dense row `orow`: itself, or -- one launch of a call split over
+// several (RgKernelArgs::out_tile_mul > 1) -- the row of the CALL's selected tile
+// (orow / tile_rows) * mul + add that this launch's tile is.
+__device__ __forceinline__ uint32_t out_row_of(const RgKernelArgs &a, uint32_t orow) {
+    if (a.out_tile_mul <= 1u) return orow;
+    const uint32_t tl = orow / a.tile_rows;
+    return (tl * a.out_tile_mul + a.out_tile_add) * a.tile_rows + (orow - tl * a.tile_rows);
+}
+
 constexpr size_t RG_NO_PIXEL = ~(size_t)0;  // a lane of a tile that lies outside the output
 
 // A wave finished tile `tile`: store its pixels (one coalesced store), then,
@@ -1457,6 +1466,9 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+#ifndef RG_GLOBAL_FRAMES
+#define RG_GLOBAL_FRAMES 0  // every path: shading frames field-major in global memory (no scratch array)
+#endif
 #ifndef RG_LIGHT_GLOBAL_FRAMES
 #define RG_LIGHT_GLOBAL_FRAMES 0  // light path: shading frames field-major in global memory instead of a scratch array
 #endif
@@ -1645,7 +1657,7 @@ __global__ __launch_bounds__(LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS, LB 
 void rg_render_kernel(RgKernelArgs a) {
     static_assert(!BVH || 4 * WPS <= RG_BVH_MAX_WAVES, "one BVH stack per wave");
     constexpr bool PLIGHT = LB > 1;  // the light path's (smaller) task pool
-    constexpr bool GFRAMES = MAXD == 0 || (LB > 1 && RG_LIGHT_GLOBAL_FRAMES);
+    constexpr bool GFRAMES = MAXD == 0 || RG_GLOBAL_FRAMES || (LB > 1 && RG_LIGHT_GLOBAL_FRAMES);
     // the launch context's other counter set (the previous launch's, read back
     // already: same stream) starts the next launch at zero -- no memset per frame
     if (blockIdx.x == 0 && a.counters_next)
@@ -1782,7 +1794,7 @@ void rg_render_kernel(RgKernelArgs a) {
             const uint32_t x = (tx << twlog) + ((uint32_t)lane & twmask);
             const uint32_t orow = ty * th + ((uint32_t)lane >> twlog);
             if (x < a.width && orow < a.out_rows) {
-                const uint32_t row = a.image_rows ? out_row_to_y(a, orow) : orow;
+                const uint32_t row = a.image_rows ? out_row_to_y(a, orow) : out_row_of(a, orow);
                 if (row != 0xFFFFFFFFu) a.rgba[(size_t)row * a.width + x] = ring_px[rw][k][lane];
             }
         }
@@ -2267,7 +2279,7 @@ void rg_render_kernel(RgKernelArgs a) {
                 const uint32_t orow = ty * th + ((uint32_t)lane >> twlog);
                 bool alive = x < a.width && orow < a.out_rows;
                 const uint32_t y = alive ? out_row_to_y(a, orow) : 0u;
-                oidx = (HOSTF && !alive) ? RG_NO_PIXEL : (size_t)orow * a.width + x;
+                oidx = (HOSTF && !alive) ? RG_NO_PIXEL : (size_t)out_row_of(a, orow) * a.width + x;
                 if (HOSTF && a.image_rows && alive)  // the whole image: the pixel's own row (padding: no store)
                     oidx = y == 0xFFFFFFFFu ? RG_NO_PIXEL : (size_t)y * a.width + x;
                 if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
@@ -2822,7 +2834,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
         *grid_threads = (size_t)blocks * threads;
         return hipSuccess;
     }
-    constexpr bool GFRAMES = MAXD == 0 || (LB > 1 && RG_LIGHT_GLOBAL_FRAMES);
+    constexpr bool GFRAMES = MAXD == 0 || RG_GLOBAL_FRAMES || (LB > 1 && RG_LIGHT_GLOBAL_FRAMES);
     if (GFRAMES && (a->deep_stack == nullptr || (unsigned long long)a->deep_stride < blocks * threads))
         return hipErrorInvalidValue;  // the caller sized the frame buffer for another grid
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), lds, stream, *a);
@@ -2931,7 +2943,7 @@ extern "C" int rg_max_array_frames(void) { return 64; }
 // host sizes it with rg_render_grid_threads)?  Depths above the arrays always;
 // light launches too when built with RG_LIGHT_GLOBAL_FRAMES (no scratch array).
 extern "C" int rg_launch_global_frames(const RgKernelArgs *a, int maxd) {
-    return maxd > rg_max_array_frames() || (RG_LIGHT_GLOBAL_FRAMES && !rg_heavy_path(*a));
+    return maxd > rg_max_array_frames() || RG_GLOBAL_FRAMES || (RG_LIGHT_GLOBAL_FRAMES && !rg_heavy_path(*a));
 }
 
 #ifndef RG_MAXD_SMALL
