@@ -1656,6 +1656,10 @@ template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH,
 __global__ __launch_bounds__(LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS, LB > 1 ? WPS : 1)
 void rg_render_kernel(RgKernelArgs a) {
     static_assert(!BVH || 4 * WPS <= RG_BVH_MAX_WAVES, "one BVH stack per wave");
+#ifdef RG_WAVE_TIMES  // diagnostic: per-wave start (before staging), staged, end (100 MHz ticks), tiles
+    const unsigned long long t_wave0 = wall_clock64();
+    uint32_t wt_tiles = 0;
+#endif
     constexpr bool PLIGHT = LB > 1;  // the light path's (smaller) task pool
     constexpr bool GFRAMES = MAXD == 0 || RG_GLOBAL_FRAMES || (LB > 1 && RG_LIGHT_GLOBAL_FRAMES);
     // the launch context's other counter set (the previous launch's, read back
@@ -1780,6 +1784,9 @@ void rg_render_kernel(RgKernelArgs a) {
     if (lane < 16) rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][lane] = 0ull;
 #endif
     [[maybe_unused]] const unsigned long long t_kernel = RG_CLOCK();
+#ifdef RG_WAVE_TIMES
+    const unsigned long long t_staged = wall_clock64();
+#endif
     const uint32_t twlog = HOSTF ? a.tile_wlog : 3u, twmask = (1u << twlog) - 1u, th = 64u >> twlog;
     const uint32_t tiles_x = (a.width + twmask) >> twlog;
     const uint32_t ntiles = tiles_x * ((a.out_rows + th - 1u) / th);
@@ -2129,7 +2136,7 @@ void rg_render_kernel(RgKernelArgs a) {
                                                 (f32_to_u8(ret.b * 255.0f) << 16) | 0xFF000000u;
                             if (HOSTF && a.defer_px) *my_px = px;
                             else a.rgba[oidx] = px;
-#ifndef RG_TILE_TIMES
+#if !defined(RG_TILE_TIMES) && !defined(RG_WAVE_TIMES)
                             if (a.rgb) { a.rgb[3 * oidx] = ret.r; a.rgb[3 * oidx + 1] = ret.g; a.rgb[3 * oidx + 2] = ret.b; }
 #endif
                         }
@@ -2267,6 +2274,9 @@ void rg_render_kernel(RgKernelArgs a) {
                     if (++tiles_taken >= kmax) tiles_left = false;
                 }
                 if (a.tile_perm) tile = a.tile_perm[tile];  // scheduling order only; every tile is rendered once
+#ifdef RG_WAVE_TIMES
+                ++wt_tiles;
+#endif
                 if constexpr (HOSTF) my_tile = tile;
                 const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
 #ifdef RG_TILE_TIMES
@@ -2285,7 +2295,7 @@ void rg_render_kernel(RgKernelArgs a) {
                 if (alive && y == 0xFFFFFFFFu) {  // padding row of a partial last tile
                     if (HOSTF && a.defer_px) *my_px = 0u;
                     else if (!HOSTF || oidx != RG_NO_PIXEL) a.rgba[oidx] = 0u;
-#ifndef RG_TILE_TIMES
+#if !defined(RG_TILE_TIMES) && !defined(RG_WAVE_TIMES)
                     if (a.rgb) { a.rgb[3 * oidx] = 0.0f; a.rgb[3 * oidx + 1] = 0.0f; a.rgb[3 * oidx + 2] = 0.0f; }
 #endif
                     alive = false;
@@ -2545,6 +2555,16 @@ void rg_render_kernel(RgKernelArgs a) {
 
     RG_STAT(14, RG_CLOCK() - t_kernel);
     RG_STAT(15, 1);
+#ifdef RG_WAVE_TIMES
+    if (lane == 0 && a.rgb) {  // wave w of the grid: 4 words at rgb[4 w]
+        const unsigned long long t_end = wall_clock64();
+        uint32_t *wt = reinterpret_cast<uint32_t *>(a.rgb) + 4u * (blockIdx.x * (blockDim.x / 64u) + (threadIdx.x >> 6));
+        wt[0] = (uint32_t)t_wave0;
+        wt[1] = (uint32_t)(t_staged - t_wave0);
+        wt[2] = (uint32_t)(t_end - t_wave0);
+        wt[3] = wt_tiles;
+    }
+#endif
 #ifdef RG_BVH_STATS
     if (lane >= 4 && lane < 16) atomicAdd(&a.counters[lane], rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][lane]);
 #endif
