@@ -42,6 +42,9 @@ extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStrea
 extern "C" hipError_t rg_render_grid_threads(const RgKernelArgs *a, int maxd, size_t *threads);
 extern "C" int rg_max_array_frames(void);
 extern "C" int rg_launch_global_frames(const RgKernelArgs *a, int maxd);
+#ifndef RG_LIGHT_SINGLE_ORDER
+#define RG_LIGHT_SINGLE_ORDER 0
+#endif
 extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scratch, uint32_t *perm, hipStream_t stream);
 extern "C" size_t rg_tile_order_scratch_words(uint32_t ntiles);
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,
@@ -373,7 +376,9 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     a.prim_sy = cx->prim + width;
     if (!rg_heavy_path(a)) a.lds_blob = lds_blob_for(s, a);  // light path: one staging loop per block
     if (timed && !ok(hipEventRecord(cx->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
-    if (s->tile_order == 1 || (s->tile_order < 0 && rg_heavy_path(a))) {
+    // expensive tiles first: the heavy path always; light single launches when built with
+    // RG_LIGHT_SINGLE_ORDER (persistent waves then start the long ray trees first)
+    if (s->tile_order == 1 || (s->tile_order < 0 && (rg_heavy_path(a) || (RG_LIGHT_SINGLE_ORDER && !pipelined)))) {
         const size_t ntiles = (size_t)rg_tile_count(a);
         const rg_launch_ctx::PermKey key{width, height, tiling->tile_rows, tiling->tile_stride, tiling->tile_offset,
                                          tile_first, out_rows, tile_wlog, s->max_depth, (uint32_t)s->n_lights,

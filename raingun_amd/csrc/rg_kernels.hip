@@ -2775,6 +2775,12 @@ extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scra
 // ---------------------------------------------------------------- launchers
 // One persistent block per CU slot: grid = CUs x (blocks per CU the register
 // and LDS budgets admit), capped by the tiles the frame has.
+#ifndef RG_LIGHT_PERSIST_BLOCKS_PER_CU
+#define RG_LIGHT_PERSIST_BLOCKS_PER_CU 16  // light persistent launches: one-wave blocks per CU (4 per SIMD)
+#endif
+#ifndef RG_DEEP_FORCE
+#define RG_DEEP_FORCE 0  // 1: host-frame / deep light launches run exactly RG_DEEP_BLOCKS_PER_CU blocks per CU
+#endif
 #ifndef RG_DEEP_BLOCKS_PER_CU
 #define RG_DEEP_BLOCKS_PER_CU 8  // deep-stack light launches: resident one-wave blocks per CU (bounds the frame buffer)
 #endif
@@ -2827,7 +2833,11 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     int cus = 0, per_cu = 0;
     const hipError_t oe = occupancy(reinterpret_cast<const void *>(kern), threads, lds, cus, per_cu);
     if (oe != hipSuccess) return oe;
-    if (MAXD == 0 && LB > 1 && per_cu > RG_DEEP_BLOCKS_PER_CU) per_cu = RG_DEEP_BLOCKS_PER_CU;
+    if (MAXD == 0 && LB > 1 && (RG_DEEP_FORCE || per_cu > RG_DEEP_BLOCKS_PER_CU)) per_cu = RG_DEEP_BLOCKS_PER_CU;
+    // light single launches, persistent waves (TPW < 0): the occupancy query answers 8 one-wave
+    // blocks per CU, while 4 waves per SIMD (128 VGPRs) are resident (RG_WAVE_TIMES: 4,050 waves
+    // of one test1 launch ran at once) -- the resident count is set explicitly
+    if (MAXD != 0 && LB > 1 && TPW < 0) per_cu = RG_LIGHT_PERSIST_BLOCKS_PER_CU;
     const unsigned long long tiles = rg_tile_count(*a);
     const unsigned long long waves = (unsigned long long)threads / 64u;
     unsigned long long blocks = (unsigned long long)cus * per_cu;
