@@ -64,6 +64,28 @@ def test_invalid_arguments_fail_loudly(libpath):
     assert out.value is None
     assert lib.rg_frames_step(None) == _abi.RG_ERR_INVALID_ARGUMENT
     assert lib.rg_frames_image(None) is None
+    px = C.c_int32(5)
+    assert lib.rg_frames_status(None, C.byref(px)) == _abi.RG_ERR_INVALID_ARGUMENT
+    assert lib.rg_frames_read_image(None, None) == _abi.RG_ERR_INVALID_ARGUMENT
+    assert lib.rg_frames_flush(None) == _abi.RG_ERR_INVALID_ARGUMENT
+
+
+def test_comm_entry_points_validate_arguments(libpath):
+    """The library's own RCCL communicator (raingun_frames.h rg_comm_*): argument
+    errors come back as status codes before any RCCL or HIP call."""
+    import ctypes as C
+    lib = _abi.lib()
+    assert lib.rg_comm_id_bytes() == 128
+    assert lib.rg_comm_unique_id(None) == _abi.RG_ERR_INVALID_ARGUMENT
+    uid = (C.c_uint8 * 128)()
+    comm = C.c_void_p(9)
+    assert lib.rg_comm_init_rank(None, 2, 0, 0, C.byref(comm)) == _abi.RG_ERR_INVALID_ARGUMENT
+    assert comm.value is None  # cleared on every failure
+    for world, rank, dev in ((0, 0, 0), (2, 2, 0), (2, -1, 0), (2, 0, -1)):
+        assert lib.rg_comm_init_rank(uid, world, rank, dev, C.byref(comm)) == _abi.RG_ERR_INVALID_ARGUMENT
+    assert lib.rg_comm_init_rank(uid, 1, 0, 0, None) == _abi.RG_ERR_INVALID_ARGUMENT
+    assert lib.rg_comm_info(None, None, None, None) == _abi.RG_ERR_INVALID_ARGUMENT
+    assert lib.rg_comm_destroy(None) == _abi.RG_ERR_INVALID_ARGUMENT
 
 
 def test_struct_sizes_match_header():
