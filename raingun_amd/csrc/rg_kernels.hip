@@ -2894,11 +2894,13 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 
 #ifndef RG_LIGHT_BIG_TPW
 // Light path, launches of at least RG_LIGHT_BIG_TILES tiles (4K frames and their halves): more
-// tiles per wave (fewer wave starts and scene stagings per frame: test1 0.2980 -> 0.2956 ms,
-// profiles/r03/late/ab_light_big_tpw.txt; 64 measures the same); smaller launches (the 1/4, 1/8
-// shares of a multi-GPU frame, host-visible bands) keep RG_LIGHT_TILES_PER_WAVE, which
-// measured faster for them.  0 = one tiles-per-wave for every launch.
-#define RG_LIGHT_BIG_TPW 32
+// tiles per wave (fewer wave starts and scene stagings per frame: round 3, 32 tiles, test1
+// 0.2980 -> 0.2956 ms over 200 frames, profiles/r03/late/ab_light_big_tpw.txt).  Round 4: a
+// launch is its slowest wave's tile chain, so 32-tile chains leave a long drain
+// at the end of a short sequence: with 16 tiles per wave the bench's 20-frame configuration runs
+// test1 0.3139 -> 0.3068 ms and test3 0.274 -> 0.2635 (200 frames: +0.6 % / equal;
+// profiles/r04/s13/session.txt).  0 = RG_LIGHT_TILES_PER_WAVE for every launch.
+#define RG_LIGHT_BIG_TPW 0
 #endif
 #ifndef RG_LIGHT_BIG_TILES
 #define RG_LIGHT_BIG_TILES 50000ull  // whole 4K frames and 1/2 shares (test1 1/2 share 0.1504 -> 0.1490 ms)
