@@ -609,6 +609,10 @@ __device__ __forceinline__ void cswap(uint32_t &x, uint32_t &y) {
 #ifndef RG_LANE_BRANCHFREE
 #define RG_LANE_BRANCHFREE 1  // per-lane walk: child slots processed without divergent branches (one spare stack slot)
 #endif
+#ifndef RG_LANE_TOP
+#define RG_LANE_TOP 0  // per-lane walk: the stack's top entry in a register (pops without an LDS read;
+                       // north star 2.4387 -> 2.4307 ms over 60 frames, 20 frames equal: within noise, off)
+#endif
 #ifndef RG_LANE_LEAF_BATCH
 #define RG_LANE_LEAF_BATCH 0  // 1: the per-lane walk postpones leaf tests and runs them in batches (below)
 #endif
@@ -707,6 +711,9 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
 #if RG_LANE_BRANCHFREE
     const uint32_t capo = (uint32_t)cap * stride;
     uint32_t spo = 0u;
+#if RG_LANE_TOP
+    uint32_t top = ~0u;  // the stack's top entry, in a register (~0: none)
+#endif
 #endif
     for (;;) {
         const bool act = need && node >= 0;
@@ -749,17 +756,49 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             cswap(e0, e1); cswap(e2, e3); cswap(e0, e2); cswap(e1, e3); cswap(e1, e2);
             // slot `cap` is a spare: a write that is not a push may land there, never on an entry;
             // the stack pointer is kept scaled by the stride (spo = sp * stride: no multiplies)
+#if RG_LANE_TOP
+            // the stack's top entry stays in a register (`top`): the entry a node visit pushes
+            // last (e1) is the one the walk most often pops next, without an LDS round trip;
+            // the previous top goes to LDS under the new pushes (LIFO order unchanged)
+            const bool p1 = e1 != ~0u;  // sorted: e2, e3 are empty when e1 is
+            stk[min(spo, capo)] = top;
+            spo += (p1 & (top != ~0u) & (spo < capo)) ? stride : 0u;
+            stk[min(spo, capo)] = e3;
+            spo += ((e3 != ~0u) & (spo < capo)) ? stride : 0u;
+            stk[min(spo, capo)] = e2;
+            spo += ((e2 != ~0u) & (spo < capo)) ? stride : 0u;
+            top = p1 ? e1 : top;
+#else
             stk[min(spo, capo)] = e3;
             spo += ((e3 != ~0u) & (spo < capo)) ? stride : 0u;
             stk[min(spo, capo)] = e2;
             spo += ((e2 != ~0u) & (spo < capo)) ? stride : 0u;
             stk[min(spo, capo)] = e1;
             spo += ((e1 != ~0u) & (spo < capo)) ? stride : 0u;
+#endif
             const float tbn = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
             if (e0 != ~0u && (shadow || !(lane_key_t(e0) > tbn))) {
                 node = (int)(e0 & mask);
             } else {
                 node = -1;
+#if RG_LANE_TOP
+                while (need) {
+                    uint32_t e;
+                    if (top != ~0u) {
+                        e = top;
+                        top = ~0u;
+                    } else if (spo > 0u) {
+                        spo -= stride;
+                        e = stk[spo];
+                    } else {
+                        break;
+                    }
+                    if (shadow || !(lane_key_t(e) > tbn)) {
+                        node = (int)(e & mask);
+                        break;
+                    }
+                }
+#else
                 while (spo > 0u && need) {
                     spo -= stride;
                     const uint32_t e = stk[spo];
@@ -768,6 +807,7 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
                         break;
                     }
                 }
+#endif
             }
         }
 #else
@@ -1224,6 +1264,22 @@ __device__ __forceinline__ C3 material_color(const RgTexDev *texs, const RgMatDe
     return c3(u8_div255(px & 0xffu), u8_div255((px >> 8) & 0xffu), u8_div255((px >> 16) & 0xffu));
 }
 
+// material_color in two halves (light path, RG_LIGHT_TEXEL_EARLY): the texel load
+// is issued at the hit and its conversion runs after the shadow batch's setup, so
+// the load's latency overlaps the per-light work instead of stalling the wave.
+__device__ __forceinline__ uint32_t texel_fetch(const RgTexDev *texs, const RgMatDev &m, const RgBodyDev &b, V3 h) {
+    float tx, ty;
+    texture_coords(b, h, tx, ty);
+    const RgTexDev t = texs[m.tex];
+    uint32_t x = wrap(tx + m.xoff, t.w);
+    uint32_t y = wrap(ty + m.yoff, t.h);
+    const __attribute__((address_space(1))) uint32_t *tg = (const __attribute__((address_space(1))) uint32_t *)t.texels;
+    return tg[(size_t)y * (uint32_t)t.w + x];
+}
+__device__ __forceinline__ C3 texel_color(uint32_t px) {
+    return c3(u8_div255(px & 0xffu), u8_div255((px >> 8) & 0xffu), u8_div255((px >> 16) & 0xffu));
+}
+
 // body.color(&body.texture_coords(hit)) (rendering.rs:134-135, 103).  The
 // texture coordinates are pure functions of the hit and only a Texture
 // coloration reads them, so they are computed for textured materials only:
@@ -1471,6 +1527,12 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 #endif
 #ifndef RG_LIGHT_GLOBAL_FRAMES
 #define RG_LIGHT_GLOBAL_FRAMES 0  // light path: shading frames field-major in global memory instead of a scratch array
+#endif
+#ifndef RG_LIGHT_TEXEL_EARLY
+// light path: a textured hit's texel load is issued at the hit and converted after the lights'
+// setup, so its latency overlaps that work (test1 0.2979 -> 0.2955 ms over 200 frames, 20 frames
+// 0.3059 -> 0.3051, test3 equal; profiles/r04/s15/session.txt)
+#define RG_LIGHT_TEXEL_EARLY 1
 #endif
 #ifndef RG_PRIO_DEPTH
 #define RG_PRIO_DEPTH 0    // > 0: waves with a query at this recursion depth or deeper run at raised priority
@@ -1900,8 +1962,17 @@ void rg_render_kernel(RgKernelArgs a) {
                             // ONE batch covers every light (n_lights <= LB on this path): set it
                             // up now, with the per-light shading factors (parked in LDS), so that
                             // no hit-point state (h, n, incident) has to survive the shadow pass
+#if RG_LIGHT_TEXEL_EARLY
+                            // a textured hit's texel load goes out now and is converted after the
+                            // lights' setup below (its latency overlaps that work)
+                            const bool textured = m.coloration != RG_COLORATION_COLOR;
+                            uint32_t texel = 0u;
+                            if (textured) texel = texel_fetch(T.texs, m, b, h);
+                            else { park[64 * PK_COL] = m.color[0]; park[64 * (PK_COL + 1)] = m.color[1]; park[64 * (PK_COL + 2)] = m.color[2]; }
+#else
                             const C3 col = surface_color(T.texs, m, b, h);
                             park[64 * PK_COL] = col.r; park[64 * (PK_COL + 1)] = col.g; park[64 * (PK_COL + 2)] = col.b;
+#endif
                             park[64 * PK_REFL] = m.albedo_pi;                       // rendering.rs:164
                             // how the batch's colour is used: 0 diffuse, 1 reflecting at the depth
                             // limit (mix with the default colour), 2 reflecting with a frame
@@ -1930,6 +2001,12 @@ void rg_render_kernel(RgKernelArgs a) {
                                     sb.ld[l] = 0.0;
                                 }
                             }
+#if RG_LIGHT_TEXEL_EARLY
+                            if (textured) {
+                                const C3 col = texel_color(texel);
+                                park[64 * PK_COL] = col.r; park[64 * (PK_COL + 1)] = col.g; park[64 * (PK_COL + 2)] = col.b;
+                            }
+#endif
                             if (a.n_lights > 0) mode = MODE_SHADOW;
                             else shade = true;  // no lights: finish with black (rendering.rs:138)
                         } else {
