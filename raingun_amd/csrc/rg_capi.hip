@@ -7,6 +7,8 @@
 // abort crosses the ABI.
 #include <hip/hip_runtime.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -240,7 +242,7 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
     a.lane_stack = lane ? s->lane_stack : 0;
     a.lane_min_depth = lane ? s->lane_min_depth : 1 << 30;
     // lane_stack entries + one spare slot per lane (rg_kernels.hip bvh_lane, RG_LANE_BRANCHFREE)
-    a.lds_lstack_bytes = lane ? (uint32_t)(a.lane_stack + 1) * 256u * RG_HEAVY_WPS * 4u : 0u;
+    a.lds_lstack_bytes = lane ? ((uint32_t)(a.lane_stack + 1) * 4u + RG_LANE_HELP_BYTES) * 256u * RG_HEAVY_WPS : 0u;
     // LDS arena: [lane stacks | sphf | sphf2 | sph | cc (padded to 16 B) | nodes | pln | dsk | box (padded) |
     //             lights | texs (padded) | bodies | mats].  The hot part (staged whenever the sphere
     //             tables are) ends after the texture descriptors: lights and texture descriptors are a
@@ -914,6 +916,41 @@ inline void piece(size_t bytes, int i, int n, size_t &off, size_t &len) {
 }
 }  // namespace
 
+#ifndef RG_COPY_NT
+#define RG_COPY_NT 0  // pageable destinations: non-temporal (streaming) stores for the band copies
+#endif
+namespace {
+// A band's copy out of pinned staging into the caller's pageable frame with
+// streaming stores: the destination lines are written whole and not read first
+// (a plain memcpy below glibc's non-temporal threshold reads every destination
+// line for ownership), and they do not evict the staging data from the caches.
+__attribute__((target("avx2"))) void copy_nt_avx2(unsigned char *dst, const unsigned char *src, size_t n) {
+    const size_t head = std::min(n, (size_t)((32u - ((uintptr_t)dst & 31u)) & 31u));
+    std::memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    size_t i = 0;
+    for (; i + 128 <= n; i += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 64));
+        const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 96), d);
+    }
+    _mm_sfence();
+    std::memcpy(dst + i, src + i, n - i);
+}
+void copy_band(unsigned char *dst, const unsigned char *src, size_t n) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (RG_COPY_NT && avx2 && n >= 4096) copy_nt_avx2(dst, src, n);
+    else std::memcpy(dst, src, n);
+}
+}  // namespace
+
 void rg_copy_pool::run(int id) {
     uint64_t seen = 0;
     for (;;) {
@@ -933,7 +970,7 @@ void rg_copy_pool::run(int id) {
         seen = g;
         size_t off, len;
         piece(p_->bytes, id, p_->parts, off, len);
-        if (len) std::memcpy(p_->dst + off, p_->src + off, len);
+        if (len) copy_band(p_->dst + off, p_->src + off, len);
         p_->remaining.fetch_sub(1, std::memory_order_acq_rel);
     }
 }
@@ -954,7 +991,7 @@ void rg_copy_pool::copy(void *dst, const void *src, size_t bytes) {
     p_->cv.notify_all();
     size_t off, len;
     piece(bytes, 0, p_->parts, off, len);
-    if (len) std::memcpy(p_->dst + off, p_->src + off, len);
+    if (len) copy_band(p_->dst + off, p_->src + off, len);
     while (p_->remaining.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
 }
 

@@ -61,6 +61,12 @@ struct alignas(16) RgBvhNode {
 // lower bound, so pruning at pop is conservative) | the child's node index.
 #define RG_LANE_NODE_BITS 12
 #define RG_LANE_STACK_MAX 16      // entries per lane the LDS arena may hold
+#ifndef RG_LANE_HELP
+#define RG_LANE_HELP 0            // per-lane walk: lanes done with their ray take subtrees of other lanes' rays
+#endif
+// LDS per thread behind the stacks for RG_LANE_HELP: the helpers' closest sphere hit of the
+// thread's ray (u64 key, u32 id code), its occlusion flag and one matching word
+#define RG_LANE_HELP_BYTES (RG_LANE_HELP ? 20u : 0u)
 
 struct RgBodyDev {         // per body, YAML order
     int32_t kind;

@@ -613,6 +613,9 @@ __device__ __forceinline__ void cswap(uint32_t &x, uint32_t &y) {
 #define RG_LANE_TOP 0  // per-lane walk: the stack's top entry in a register (pops without an LDS read;
                        // north star 2.4387 -> 2.4307 ms over 60 frames, 20 frames equal: within noise, off)
 #endif
+#ifndef RG_LANE_CLOCK_WORD
+#define RG_LANE_CLOCK_WORD 12  // RG_BVH_STATS: counter word of the per-lane walk's clock (13: apart from the wave walk's)
+#endif
 #ifndef RG_LANE_LEAF_BATCH
 #define RG_LANE_LEAF_BATCH 0  // 1: the per-lane walk postpones leaf tests and runs them in batches (below)
 #endif
@@ -875,8 +878,252 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
 #endif
     }
 #endif
-    RG_STAT(12, RG_CLOCK() - t_in);
+    RG_STAT(RG_LANE_CLOCK_WORD, RG_CLOCK() - t_in);
 }
+
+#if RG_LANE_HELP
+// Per-lane walk with helpers (RG_LANE_HELP).  The lanes of a wave finish their
+// walks at different times; in bvh_lane the finished ones idle until the
+// wave's longest walk is done (25 of 64 lanes active per iteration on the
+// north star).  Here, whenever few lanes are still walking, a balancing step
+// lets every idle lane -- done with its ray, or never given one -- take the
+// BOTTOM entry of a walking lane's stack (the shallowest deferred subtree) and
+// walk that subtree for the walking lane's ray: the ray (o, d, light distance,
+// start offset, current closest hit as the bound) comes over ds_bpermute, the
+// subtree is walked with the helper's own stack.  A helper's finds go to the
+// ray's result slot in LDS: closest sphere hit as an atomic min over (key =
+// t's bits without the sign, then code = id << 1 | sign bit), occlusion as a
+// flag; walking lanes fold their ray's slot into their bound at every step.
+// The accepted set is what bvh_lane accepts (same boxes and leaf tests; a
+// subtree skipped only when its entry distance exceeds a bound that is a
+// closest hit the ray really has), and the closest-hit rule is an
+// order-independent lexicographic minimum, so the result is identical.
+#ifndef RG_HELP_ACTIVE
+#define RG_HELP_ACTIVE 40  // a balancing step runs when at most this many lanes walk ...
+#endif
+#ifndef RG_HELP_MIN_IDLE
+#define RG_HELP_MIN_IDLE 8  // ... at least this many could help, and some walking lane has a deferred subtree
+#endif
+__device__ __forceinline__ unsigned long long help_ld64(unsigned long long *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+__device__ __forceinline__ uint32_t help_ld32(uint32_t *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+__device__ __forceinline__ void help_st64(unsigned long long *p, unsigned long long v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
+__device__ __forceinline__ void help_st32(uint32_t *p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
+__device__ __forceinline__ uint32_t help_pull(int src_lane, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+__device__ __forceinline__ double help_pull_d(int src_lane, double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const uint32_t lo = help_pull(src_lane, (uint32_t)b), hi = help_pull(src_lane, (uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// closest-hit rule (closest_add without the count) on (t, id)
+__device__ __forceinline__ void help_fold(double &ct, int &cid, double t, int id) {
+    if (id >= 0 && (cid < 0 || t < ct || (t == ct && id < cid))) { ct = t; cid = id; }
+}
+
+template <class Src>
+__device__ __forceinline__ void bvh_lane_help(const RgKernelArgs &a, const Src &src, const V3 o_in, const V3 d_in,
+                                              bool shadow_in, double ld_in, double t0s_in, Closest &c_in,
+                                              bool &occl_in, bool &need_in, bool mine) {
+    const uint32_t stride = blockDim.x;
+    uint32_t *stk = reinterpret_cast<uint32_t *>(rg_dyn_smem) + threadIdx.x;  // entry e at stk[e * stride]
+    const uint32_t capo = (uint32_t)a.lane_stack * stride;
+    const uint32_t mask = (1u << RG_LANE_NODE_BITS) - 1u;
+    const int lane = (int)(threadIdx.x & 63u);
+    const uint32_t wbase = threadIdx.x & ~63u;
+    // behind the stacks (+ spare slot): u64 keys, u32 id codes, u32 flags, u32 matching words
+    unsigned long long *slot_t =
+        reinterpret_cast<unsigned long long *>(rg_dyn_smem + (size_t)(a.lane_stack + 1) * stride * 4u) + wbase;
+    uint32_t *slot_i = reinterpret_cast<uint32_t *>(slot_t - wbase + stride) + wbase;
+    uint32_t *slot_o = slot_i + stride;
+    uint32_t *match = slot_o + stride;
+    help_st64(&slot_t[lane], ~0ull);
+    help_st32(&slot_i[lane], ~0u);
+    help_st32(&slot_o[lane], 0u);
+    const int nexec = __builtin_popcountll(__ballot(1));
+
+    // the lane's current walk (its own ray, or a subtree of another lane's ray for `owner`)
+    V3 o = o_in, d = d_in;
+    bool shadow = shadow_in;
+    double ld = ld_in, t0s = t0s_in;
+    double ct = c_in.t;
+    int cid = c_in.id;
+    bool need = mine && need_in, occl = false;
+    bool open = need;
+    int owner = lane;
+    // the lane's own ray once its own walk is done
+    double rt = c_in.t;
+    int rid = c_in.id;
+    bool rocc = false;
+    RayB rb;
+    RayF rf;
+    float tld;
+    auto setup = [&]() {
+        const V3 ob = t0s > 0.0 ? add(o, scl(d, t0s)) : o;
+        rb = rg_make_rayb(ob.x, ob.y, ob.z, d.x, d.y, d.z);
+        rf = make_rayf(o, d);
+        tld = shadow ? bvh_bound(ld - t0s) : 0.0f;
+    };
+    setup();
+    int node = 0;
+    uint32_t spo = 0u, boto = 0u;  // stack [boto, spo), scaled by the stride
+    RG_STAT(4, 1);
+    RG_STAT(7, RG_LANES(need));
+    [[maybe_unused]] const unsigned long long t_in = RG_CLOCK();
+    for (;;) {
+        const bool act = open && need && node >= 0;
+        const int nact = __builtin_popcountll(__ballot(act));
+        const bool donor = act && spo > boto;
+        const unsigned long long dm = __ballot(donor);
+        if (nact == 0 || (nact <= RG_HELP_ACTIVE && nexec - nact >= RG_HELP_MIN_IDLE && dm != 0ull)) {
+            // ---- balancing step (wave-uniform)
+            // 1. retire finished walks: the own ray's result stays in registers, a helper's goes
+            //    to its ray's slot (atomic min on the key; the id code is reset when the key drops)
+            const bool fin = open && !act;
+            if (fin && owner == lane) { rt = ct; rid = cid; rocc = occl; }
+            const bool put = fin && owner != lane && !shadow && cid >= 0 && !(ct < 0.0);
+            const unsigned long long key = (unsigned long long)__double_as_longlong(ct) & 0x7FFFFFFFFFFFFFFFull;
+            const uint32_t code = ((uint32_t)cid << 1) | (uint32_t)(__double_as_longlong(ct) < 0);
+            if (fin && owner != lane && occl) help_st32(&slot_o[owner], 1u);
+            unsigned long long told = 0ull;
+            if (put) told = help_ld64(&slot_t[owner]);
+            if (put) atomicMin(&slot_t[owner], key);
+            unsigned long long tnew = 0ull;
+            if (put) tnew = help_ld64(&slot_t[owner]);
+            if (put && key == tnew && tnew < told) help_st32(&slot_i[owner], ~0u);
+            if (put && key == tnew) atomicMin(&slot_i[owner], code);
+            if (fin) open = false;
+            if (nact == 0) break;
+            // 2. walking lanes fold their ray's slot into their bound (a shadow ray another lane
+            //    found occluded stops)
+            if (open) {
+                if (shadow) {
+                    if (help_ld32(&slot_o[owner]) != 0u) { occl = true; need = false; }
+                } else {
+                    const unsigned long long st = help_ld64(&slot_t[owner]);
+                    if (st != ~0ull) {
+                        const uint32_t sc = help_ld32(&slot_i[owner]);
+                        help_fold(ct, cid, __longlong_as_double((long long)(st | ((unsigned long long)(sc & 1u) << 63))),
+                                  (int)(sc >> 1));
+                    }
+                }
+            }
+            // 3. idle lane of rank i takes the bottom stack entry of the walking lane of rank i
+            const bool idle = !open;
+            const bool don = open && need && node >= 0 && spo > boto;
+            const unsigned long long im = __ballot(idle), dm2 = __ballot(don);
+            const int k = min(__builtin_popcountll(im), __builtin_popcountll(dm2));
+            if (k > 0) {
+                const int ri = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+                const int rd = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(dm2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm2, 0u));
+                const bool robbed = don && rd < k, steal = idle && ri < k;
+                if (robbed) help_st32(&match[rd], (uint32_t)lane);
+                int dl = lane;
+                if (steal) dl = (int)help_ld32(&match[ri]);
+                const uint32_t bent = stk[min(boto, capo)];
+                const uint32_t e = help_pull(dl, bent);
+                const V3 no = v3(help_pull_d(dl, o.x), help_pull_d(dl, o.y), help_pull_d(dl, o.z));
+                const V3 nd = v3(help_pull_d(dl, d.x), help_pull_d(dl, d.y), help_pull_d(dl, d.z));
+                const double nld = help_pull_d(dl, ld), nt0s = help_pull_d(dl, t0s), nct = help_pull_d(dl, ct);
+                const int ncid = (int)help_pull(dl, (uint32_t)cid);
+                const uint32_t nos = help_pull(dl, (uint32_t)owner | (shadow ? 0x100u : 0u));
+                if (robbed) boto += stride;
+                if (steal) {
+                    o = no;
+                    d = nd;
+                    ld = nld;
+                    t0s = nt0s;
+                    ct = nct;
+                    cid = ncid;
+                    owner = (int)(nos & 0xFFu);
+                    shadow = (nos & 0x100u) != 0u;
+                    occl = false;
+                    need = true;
+                    open = true;
+                    spo = 0u;
+                    boto = 0u;
+                    setup();
+                    const float tb = shadow ? tld : (cid >= 0 ? bvh_bound(ct - t0s) : __builtin_huge_valf());
+                    node = (shadow || !(lane_key_t(e) > tb)) ? (int)(e & mask) : -1;
+                }
+            }
+        }
+        if (!(open && need && node >= 0)) continue;
+        RG_STAT(5, 1);
+#ifdef RG_ITER_STATS  // per-lane walk: iterations, active lanes (counters[12..13])
+        {
+            const unsigned long long m = __ballot(1);
+            if ((int)(threadIdx.x & 63u) == __builtin_ffsll((long long)m) - 1) {
+                atomicAdd(&a.counters[12], 1ull);
+                atomicAdd(&a.counters[13], (unsigned long long)__builtin_popcountll(m));
+            }
+        }
+#endif
+        // one node (bvh_lane, RG_LANE_BRANCHFREE)
+        const RgBvhNode N = src.getn(node);
+        const float tb = shadow ? tld : (cid >= 0 ? bvh_bound(ct - t0s) : __builtin_huge_valf());
+        uint32_t e[4], leaves = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float tn = 0.0f;
+            const bool h = (k < N.nchild) & rg_child_hit(N, k, rb, tb, tn);
+            const int ch = N.child[k];
+            leaves |= (h & (ch < 0)) ? (1u << k) : 0u;
+            e[k] = (h & (ch >= 0)) ? lane_key(tn, ch) : ~0u;
+        }
+        Closest c;
+        c.t = ct;
+        c.id = cid;
+        c.nhit = 0;
+        c.nan = false;
+        while (leaves != 0u && need) {
+            const uint32_t k = (uint32_t)__builtin_ctz(leaves);
+            leaves &= leaves - 1u;
+            const int v = ~(k == 0u ? N.child[0] : k == 1u ? N.child[1] : k == 2u ? N.child[2] : N.child[3]);
+            leaf_query(a, src, v >> 3, (v & 7) + 1, o, d, rf, shadow, ld, c, occl, need);
+        }
+        ct = c.t;
+        cid = c.id;
+        uint32_t e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
+        cswap(e0, e1); cswap(e2, e3); cswap(e0, e2); cswap(e1, e3); cswap(e1, e2);
+        stk[min(spo, capo)] = e3;
+        spo += ((e3 != ~0u) & (spo < capo)) ? stride : 0u;
+        stk[min(spo, capo)] = e2;
+        spo += ((e2 != ~0u) & (spo < capo)) ? stride : 0u;
+        stk[min(spo, capo)] = e1;
+        spo += ((e1 != ~0u) & (spo < capo)) ? stride : 0u;
+        const float tbn = shadow ? tld : (cid >= 0 ? bvh_bound(ct - t0s) : __builtin_huge_valf());
+        if (e0 != ~0u && (shadow || !(lane_key_t(e0) > tbn))) {
+            node = (int)(e0 & mask);
+        } else {
+            node = -1;
+            while (spo > boto && need) {
+                spo -= stride;
+                const uint32_t en = stk[spo];
+                if (shadow || !(lane_key_t(en) > tbn)) {
+                    node = (int)(en & mask);
+                    break;
+                }
+            }
+        }
+    }
+    if (mine) {  // the own walk's result and what helpers found for this ray
+        const unsigned long long st = help_ld64(&slot_t[lane]);
+        if (st != ~0ull) {
+            const uint32_t sc = help_ld32(&slot_i[lane]);
+            help_fold(rt, rid, __longlong_as_double((long long)(st | ((unsigned long long)(sc & 1u) << 63))), (int)(sc >> 1));
+        }
+        rocc = rocc || help_ld32(&slot_o[lane]) != 0u;
+        c_in.t = rt;
+        c_in.id = rid;
+        if (rocc) {
+            occl_in = true;
+            need_in = false;
+        }
+    }
+    RG_STAT(RG_LANE_CLOCK_WORD, RG_CLOCK() - t_in);
+}
+#endif
 
 template <bool F32F, bool BVH, class Src>
 __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
@@ -1007,9 +1254,13 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
 #else
         const bool per_lane = ok && !grown && lane_walk && a.lane_stack > 0;  // incoherent rays
 #endif
+#if RG_LANE_HELP
+        if (__any(per_lane)) bvh_lane_help(a, src, o, d, shadow, ld, t0s, c, occl, need, per_lane);
+#else
         if (per_lane) {
             bvh_lane(a, src, o, d, shadow, ld, t0s, c, occl, need);
         }
+#endif
         if (ok && !grown && !per_lane) {
             bvh_spheres<1>(a, src, o, d, shadow, ld, t0s, c, occl, need);
         }
@@ -1528,6 +1779,12 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 #ifndef RG_LIGHT_GLOBAL_FRAMES
 #define RG_LIGHT_GLOBAL_FRAMES 0  // light path: shading frames field-major in global memory instead of a scratch array
 #endif
+#ifndef RG_TILE_PREFETCH
+#define RG_TILE_PREFETCH 0  // device-resident launches: the next tile's queue slot is claimed at a tile's start
+#endif
+#ifndef RG_UNWIND_PRELOAD
+#define RG_UNWIND_PRELOAD 0  // unwind: a frame's kind and first four words read together
+#endif
 #ifndef RG_LIGHT_TEXEL_EARLY
 // light path: a textured hit's texel load is issued at the hit and converted after the lights'
 // setup, so its latency overlaps that work (test1 0.2979 -> 0.2955 ms over 200 frames, 20 frames
@@ -1915,6 +2172,10 @@ void rg_render_kernel(RgKernelArgs a) {
     uint32_t pixel = 0;        // image pixel index (error reports) of the lane's pixel or task
     int task = -1;             // pool slot whose subtree this lane computes (-1: its own pixel)
     bool tiles_left = true;    // the tile queue has not been found empty
+#if RG_TILE_PREFETCH
+    [[maybe_unused]] uint32_t pf_k = 0u;       // lane 0: the prefetched slot of head qi
+    [[maybe_unused]] bool pf_valid = false;    // (wave-uniform) a slot is claimed
+#endif
     uint32_t my_tile = 0xFFFFFFFFu;  // the wave's current tile (published when done: a.tile_flags)
     [[maybe_unused]] uint32_t tiles_taken = 0;
     [[maybe_unused]] bool counted = false;  // this wave is counted in pool_of<PLIGHT>().busy
@@ -2253,10 +2514,21 @@ void rg_render_kernel(RgKernelArgs a) {
                             continue;
                         }
                     }
+#if RG_UNWIND_PRELOAD
+                    // one memory round trip for the common frame: its kind and the reflection
+                    // frame's four words are read together, before the branch on the kind
+                    const int ftype0 = f.type;
+                    const float g0 = f.f[0], g1 = f.f[1], g2 = f.f[2], g3 = f.f[3];
+                    if (ftype0 == FR_REFL) {
+                        ret = cadd(cscl(c3(g0, g1, g2), 1.0f - g3), cscl(ret, g3));
+                        sp--;
+                    } else if (ftype0 == FR_REFR_T) {
+#else
                     if (f.type == FR_REFL) {
                         ret = cadd(cscl(c3(f.f[0], f.f[1], f.f[2]), 1.0f - f.f[3]), cscl(ret, f.f[3]));
                         sp--;
                     } else if (f.type == FR_REFR_T) {
+#endif
                         f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
                         f.type = FR_REFR_R;
                         q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
@@ -2312,6 +2584,17 @@ void rg_render_kernel(RgKernelArgs a) {
             // ring mode: the queue hands out groups of RING consecutive tiles (one contiguous
             // run of host memory per ring flush: 4 KB with 64x1 tiles)
             const uint32_t qlimit = (RING > 0 && use_ring) ? (ntiles + RING - 1) / RING : ntiles;
+#if RG_TILE_PREFETCH
+            if constexpr (!HOSTF) {
+                if (pf_valid) {  // the slot claimed at the previous tile's start
+                    const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)pf_k, 0, 64));
+                    const unsigned long long t = (unsigned long long)k * RG_NQ + qi;
+                    if (t < qlimit) tile = (uint32_t)t;
+                    else { qi = (qi + 1) % RG_NQ; ++qtried; }  // that head is drained
+                    pf_valid = false;
+                }
+            }
+#endif
             while (tile == 0xFFFFFFFFu && qtried < RG_NQ) {
                 uint32_t k = 0;
                 if (lane == 0) k = atomicAdd(reinterpret_cast<unsigned int *>(&a.counters[RG_QUEUE_BASE + RG_QUEUE_STRIDE * qi]), 1u);
@@ -2350,6 +2633,18 @@ void rg_render_kernel(RgKernelArgs a) {
                     // drains through the hardware dispatcher wave (block) by wave
                     if (++tiles_taken >= kmax) tiles_left = false;
                 }
+#if RG_TILE_PREFETCH
+                if constexpr (!HOSTF) {
+                    // claim the wave's NEXT queue slot now: the atomic's round trip overlaps this
+                    // tile's work instead of stalling the wave between tiles (the wave renders
+                    // the claimed tile, or finds the head drained, at its next tile start)
+                    if (tiles_left) {
+                        if (lane == 0)
+                            pf_k = atomicAdd(reinterpret_cast<unsigned int *>(&a.counters[RG_QUEUE_BASE + RG_QUEUE_STRIDE * qi]), 1u);
+                        pf_valid = true;
+                    }
+                }
+#endif
                 if (a.tile_perm) tile = a.tile_perm[tile];  // scheduling order only; every tile is rendered once
 #ifdef RG_WAVE_TIMES
                 ++wt_tiles;
@@ -3085,7 +3380,7 @@ extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays,
                                       int32_t *body, hipStream_t stream) {
     dim3 grid((n + 255) / 256);
     // per-lane walk stacks (stride = block size): lane_stack entries + the spare slot
-    const size_t lds = a->lane_stack > 0 ? (size_t)(a->lane_stack + 1) * 256u * 4u : 0u;
+    const size_t lds = a->lane_stack > 0 ? ((size_t)(a->lane_stack + 1) * 4u + RG_LANE_HELP_BYTES) * 256u : 0u;
     hipLaunchKernelGGL(rg_trace_kernel, grid, dim3(256), lds, stream, *a, rays, n, dist, body);
     return hipGetLastError();
 }
