@@ -904,6 +904,13 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
 #ifndef RG_HELP_MIN_IDLE
 #define RG_HELP_MIN_IDLE 8  // ... at least this many could help, and some walking lane has a deferred subtree
 #endif
+#ifndef RG_HELP_ROUNDS
+#define RG_HELP_ROUNDS 1  // matching rounds per balancing step
+#endif
+// The slots are read by other lanes than the ones that wrote them: relaxed atomics on
+// different addresses may be reordered by the compiler, so a step's writes and the next
+// step's reads are separated by a fence (one wave: LDS executes its operations in order)
+__device__ __forceinline__ void help_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
 __device__ __forceinline__ unsigned long long help_ld64(unsigned long long *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 __device__ __forceinline__ uint32_t help_ld32(uint32_t *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 __device__ __forceinline__ void help_st64(unsigned long long *p, unsigned long long v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -951,10 +958,6 @@ __device__ __forceinline__ void bvh_lane_help(const RgKernelArgs &a, const Src &
     bool need = mine && need_in, occl = false;
     bool open = need;
     int owner = lane;
-    // the lane's own ray once its own walk is done
-    double rt = c_in.t;
-    int rid = c_in.id;
-    bool rocc = false;
     RayB rb;
     RayF rf;
     float tld;
@@ -977,14 +980,14 @@ __device__ __forceinline__ void bvh_lane_help(const RgKernelArgs &a, const Src &
         const unsigned long long dm = __ballot(donor);
         if (nact == 0 || (nact <= RG_HELP_ACTIVE && nexec - nact >= RG_HELP_MIN_IDLE && dm != 0ull)) {
             // ---- balancing step (wave-uniform)
-            // 1. retire finished walks: the own ray's result stays in registers, a helper's goes
-            //    to its ray's slot (atomic min on the key; the id code is reset when the key drops)
+            // 1. retire finished walks into their ray's slot (atomic min on the key; the id code
+            //    is reset when the key drops).  Every hit distance is >= 0 or -0 (bodies.rs
+            //    tests), so the key orders them as doubles do.
             const bool fin = open && !act;
-            if (fin && owner == lane) { rt = ct; rid = cid; rocc = occl; }
-            const bool put = fin && owner != lane && !shadow && cid >= 0 && !(ct < 0.0);
+            const bool put = fin && !shadow && cid >= 0 && !(ct < 0.0);
             const unsigned long long key = (unsigned long long)__double_as_longlong(ct) & 0x7FFFFFFFFFFFFFFFull;
             const uint32_t code = ((uint32_t)cid << 1) | (uint32_t)(__double_as_longlong(ct) < 0);
-            if (fin && owner != lane && occl) help_st32(&slot_o[owner], 1u);
+            if (fin && occl) help_st32(&slot_o[owner], 1u);
             unsigned long long told = 0ull;
             if (put) told = help_ld64(&slot_t[owner]);
             if (put) atomicMin(&slot_t[owner], key);
@@ -992,6 +995,7 @@ __device__ __forceinline__ void bvh_lane_help(const RgKernelArgs &a, const Src &
             if (put) tnew = help_ld64(&slot_t[owner]);
             if (put && key == tnew && tnew < told) help_st32(&slot_i[owner], ~0u);
             if (put && key == tnew) atomicMin(&slot_i[owner], code);
+            help_fence();  // the slots' updates by every lane before any lane reads them
             if (fin) open = false;
             if (nact == 0) break;
             // 2. walking lanes fold their ray's slot into their bound (a shadow ray another lane
@@ -1009,15 +1013,18 @@ __device__ __forceinline__ void bvh_lane_help(const RgKernelArgs &a, const Src &
                 }
             }
             // 3. idle lane of rank i takes the bottom stack entry of the walking lane of rank i
-            const bool idle = !open;
-            const bool don = open && need && node >= 0 && spo > boto;
-            const unsigned long long im = __ballot(idle), dm2 = __ballot(don);
-            const int k = min(__builtin_popcountll(im), __builtin_popcountll(dm2));
-            if (k > 0) {
+            //    (RG_HELP_ROUNDS times: a lone ray's deferred subtrees go to several helpers)
+            for (int round = 0; round < RG_HELP_ROUNDS; ++round) {
+                const bool idle = !open;
+                const bool don = open && need && node >= 0 && spo > boto;
+                const unsigned long long im = __ballot(idle), dm2 = __ballot(don);
+                const int k = min(__builtin_popcountll(im), __builtin_popcountll(dm2));
+                if (k == 0) break;
                 const int ri = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
                 const int rd = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(dm2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm2, 0u));
                 const bool robbed = don && rd < k, steal = idle && ri < k;
                 if (robbed) help_st32(&match[rd], (uint32_t)lane);
+                help_fence();
                 int dl = lane;
                 if (steal) dl = (int)help_ld32(&match[ri]);
                 const uint32_t bent = stk[min(boto, capo)];
@@ -1107,16 +1114,15 @@ __device__ __forceinline__ void bvh_lane_help(const RgKernelArgs &a, const Src &
             }
         }
     }
-    if (mine) {  // the own walk's result and what helpers found for this ray
+    help_fence();
+    if (mine) {  // what the own walk and the helpers found for this ray
         const unsigned long long st = help_ld64(&slot_t[lane]);
         if (st != ~0ull) {
             const uint32_t sc = help_ld32(&slot_i[lane]);
-            help_fold(rt, rid, __longlong_as_double((long long)(st | ((unsigned long long)(sc & 1u) << 63))), (int)(sc >> 1));
+            c_in.t = __longlong_as_double((long long)(st | ((unsigned long long)(sc & 1u) << 63)));
+            c_in.id = (int)(sc >> 1);
         }
-        rocc = rocc || help_ld32(&slot_o[lane]) != 0u;
-        c_in.t = rt;
-        c_in.id = rid;
-        if (rocc) {
+        if (help_ld32(&slot_o[lane]) != 0u) {
             occl_in = true;
             need_in = false;
         }
@@ -1780,7 +1786,12 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 #define RG_LIGHT_GLOBAL_FRAMES 0  // light path: shading frames field-major in global memory instead of a scratch array
 #endif
 #ifndef RG_TILE_PREFETCH
-#define RG_TILE_PREFETCH 0  // device-resident launches: the next tile's queue slot is claimed at a tile's start
+// light path, device-resident launches: the next tile's queue slot is claimed at a tile's
+// start (round 4, same box, interleaved: test1 0.2972 -> 0.2939 ms over 200 frames, 0.3056 ->
+// 0.3043 over 20, test3 0.2656 -> 0.2631 over 20: profiles/r04/s21/session.txt, s22).  Not on
+// the heavy path: a claimed tile waits behind the wave's current (long) one, which lengthens
+// the frame's tail (north star 2.449 -> 2.463 ms)
+#define RG_TILE_PREFETCH 1
 #endif
 #ifndef RG_UNWIND_PRELOAD
 #define RG_UNWIND_PRELOAD 0  // unwind: a frame's kind and first four words read together
@@ -2585,7 +2596,7 @@ void rg_render_kernel(RgKernelArgs a) {
             // run of host memory per ring flush: 4 KB with 64x1 tiles)
             const uint32_t qlimit = (RING > 0 && use_ring) ? (ntiles + RING - 1) / RING : ntiles;
 #if RG_TILE_PREFETCH
-            if constexpr (!HOSTF) {
+            if constexpr (!HOSTF && LB > 1) {
                 if (pf_valid) {  // the slot claimed at the previous tile's start
                     const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)pf_k, 0, 64));
                     const unsigned long long t = (unsigned long long)k * RG_NQ + qi;
@@ -2634,7 +2645,7 @@ void rg_render_kernel(RgKernelArgs a) {
                     if (++tiles_taken >= kmax) tiles_left = false;
                 }
 #if RG_TILE_PREFETCH
-                if constexpr (!HOSTF) {
+                if constexpr (!HOSTF && LB > 1) {
                     // claim the wave's NEXT queue slot now: the atomic's round trip overlaps this
                     // tile's work instead of stalling the wave between tiles (the wave renders
                     // the claimed tile, or finds the head drained, at its next tile start)
