@@ -1767,6 +1767,12 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 #ifndef RG_LIGHT_TILES_PER_WAVE
 #define RG_LIGHT_TILES_PER_WAVE 16
 #endif
+#ifndef RG_LIGHT_CAP_MUL
+// light path, device-resident launches: a wave may take this many times its share of tiles
+// (the grid is still sized by the share), so waves whose tiles are cheap take more of them and
+// the queue drains evenly instead of every wave rendering exactly its share
+#define RG_LIGHT_CAP_MUL 1
+#endif
 #ifndef RG_HEAVY_TILES_PER_WAVE
 #define RG_HEAVY_TILES_PER_WAVE 0  // heavy path: 0 = persistent blocks (one per CU)
 #endif
@@ -2637,7 +2643,8 @@ void rg_render_kernel(RgKernelArgs a) {
             if (tile == 0xFFFFFFFFu) {
                 tiles_left = false;
             } else {
-                constexpr uint32_t kmax = MAXD == 0 || TPW < 0 ? 0u : LB > 1 ? (TPW > 0 ? (uint32_t)TPW : RG_LIGHT_TILES_PER_WAVE)
+                constexpr uint32_t kmax = MAXD == 0 || TPW < 0 ? 0u : LB > 1 ? (TPW > 0 ? (uint32_t)TPW : RG_LIGHT_TILES_PER_WAVE) *
+                                                                          (HOSTF ? 1u : (uint32_t)RG_LIGHT_CAP_MUL)
                                                                  : RG_HEAVY_TILES_PER_WAVE;
                 if constexpr (kmax > 0) {
                     // non-persistent: a wave renders at most kmax tiles, so the grid
