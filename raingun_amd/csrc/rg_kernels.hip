@@ -153,6 +153,7 @@ __device__ __forceinline__ bool disk_hit(const RgDsk &k, V3 o, V3 d, double &t) 
 //  * SphScalar: scalar loads through the constant address space (s_load,
 //    SGPR operands) for scenes whose tables exceed the LDS budget.
 struct SphScalar {
+    static constexpr bool in_lds = false;
     const RG_CONST RgSph *s;
     const RG_CONST double *cc;
     const RG_CONST RgSphF *f;
@@ -173,6 +174,7 @@ struct SphScalar {
     __device__ __forceinline__ RgSphF2 getf2(int i) const { return f2[i]; }
 };
 struct SphLds {
+    static constexpr bool in_lds = true;
     const RgSph *s;
     const double *cc;
     const RgSphF *f;
@@ -479,15 +481,43 @@ __device__ __forceinline__ void leaf_primary(const RgKernelArgs &a, const Src &s
     }
 }
 
+#ifndef RG_LEAF_PREFETCH
+#define RG_LEAF_PREFETCH 0  // BVH leaf tests on global sphere tables: the next sphere's filter records read ahead
+#endif
 template <class Src>
 __device__ __forceinline__ void leaf_query(const RgKernelArgs &a, const Src &src, int first, int count, V3 o, V3 d,
                                            const RayF &rf, bool shadow, double ld, Closest &c, bool &occl,
                                            bool &need) {
+    // RG_LEAF_PREFETCH, sphere tables in global memory (scenes too large for LDS): the next
+    // sphere's filter records are read before this sphere's tests, so their round trip overlaps
+    // the filter and the exact test.  Off: the configs[4] line at 16384^2 is unchanged (206.28
+    // vs 206.30 ms; 5-frame 1080p samples -3..-6 %, within their noise); from LDS the extra
+    // registers cost more than the overlap saves (north star 2.448 -> 2.532 ms, 6 -> 13
+    // spilled VGPRs; profiles/r04/s24, s25)
+    constexpr bool PF = RG_LEAF_PREFETCH && !Src::in_lds;
+    RgSphF fn;
+    RgSphF2 f2n;
+    if constexpr (PF) {
+        fn = src.getf(first);
+        f2n = src.getf2(first);
+    }
     for (int j = first; j < first + count; ++j) {
         // the id comes with the filter record (RgSphF2::id): a per-lane j (bvh_lane) would
         // otherwise make sph_id[j] a vector global load whose latency the hit waits for
-        const RgSphF2 f2 = src.getf2(j);
-        if (need && filter_general(src.getf(j), f2, rf)) {
+        RgSphF f;
+        RgSphF2 f2;
+        if constexpr (PF) {
+            f = fn;
+            f2 = f2n;
+            if (j + 1 < first + count) {
+                fn = src.getf(j + 1);
+                f2n = src.getf2(j + 1);
+            }
+        } else {
+            f = src.getf(j);
+            f2 = src.getf2(j);
+        }
+        if (need && filter_general(f, f2, rf)) {
             const RgSph s = src.get(j);
             const double hx = s.cx - o.x, hy = s.cy - o.y, hz = s.cz - o.z;
             const double adj = (hx * d.x + hy * d.y) + hz * d.z;
