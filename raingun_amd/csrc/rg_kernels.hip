@@ -3354,7 +3354,8 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
             // a launch on its own (not one of several frames in flight): persistent waves at full
             // occupancy balance the tiles dynamically, where a fixed tiles-per-wave grid makes every
             // wave render exactly that many tiles and the slowest wave's sum the makespan
-            if (!a->pipelined)
+            // (2: launches below RG_LIGHT_BIG_TILES tiles only -- rg_render_multi's shares and bands)
+            if (!a->pipelined && (RG_LIGHT_SINGLE_PERSISTENT != 2 || rg_tile_count(*a) < RG_LIGHT_BIG_TILES))
                 return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, RG_LIGHT_F32_FILTER, false, RG_LIGHT_TASKS, -1>(a, stream, gt);
         }
         if constexpr (MAXD != 0 && RG_LIGHT_LATENCY_TASKS && !RG_LIGHT_TASKS) {
