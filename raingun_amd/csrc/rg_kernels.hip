@@ -3196,7 +3196,7 @@ extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scra
 // One persistent block per CU slot: grid = CUs x (blocks per CU the register
 // and LDS budgets admit), capped by the tiles the frame has.
 #ifndef RG_LIGHT_PERSIST_BLOCKS_PER_CU
-#define RG_LIGHT_PERSIST_BLOCKS_PER_CU 16  // light persistent launches: one-wave blocks per CU (4 per SIMD)
+#define RG_LIGHT_PERSIST_BLOCKS_PER_CU 8  // light persistent launches: one-wave blocks per CU (2 per SIMD)
 #endif
 #ifndef RG_DEEP_FORCE
 #define RG_DEEP_FORCE 0  // 1: host-frame / deep light launches run exactly RG_DEEP_BLOCKS_PER_CU blocks per CU
@@ -3326,7 +3326,11 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 #define RG_LIGHT_BIG_TILES 50000ull  // whole 4K frames and 1/2 shares (test1 1/2 share 0.1504 -> 0.1490 ms)
 #endif
 #ifndef RG_LIGHT_SINGLE_PERSISTENT
-#define RG_LIGHT_SINGLE_PERSISTENT 0  // light path: single launches run persistent waves (TPW < 0)
+// light path: single launches run persistent waves (TPW < 0); 2: only launches below
+// RG_LIGHT_BIG_TILES (rg_render_multi's shares and bands), at 2 waves per SIMD -- test1 1/8
+// share 0.183 -> 0.166 ms, its 8-device rehearsal 0.3175 -> 0.297 ms (2.8x -> 3.0x); test3
+// equal; 3 waves per SIMD: no gain (profiles/r04/s27/session.txt)
+#define RG_LIGHT_SINGLE_PERSISTENT 2
 #endif
 #ifndef RG_LIGHT_LATENCY_TASKS
 #define RG_LIGHT_LATENCY_TASKS 0  // light path: task splitting for single small launches (below RG_LIGHT_TASK_TILES)
