@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-4 measurement session at HEAD (small single launches on persistent light waves): the whole -m gpu suite and smoke(), the
-# default bench line (every extra line, CPU baseline), the driver's configuration
-# (--steps 20 --warmup 5), the rocprofv3 kernel-trace summary of the default main
-# line, then the executed-work PMC passes of the main bench lines.
+# Round-4 measurement session at HEAD (small single launches on persistent light
+# waves): the whole -m gpu suite and smoke(), the default bench line (every
+# extra line, CPU baseline), the driver's configuration (--steps 20 --warmup 5)
+# and the rocprofv3 kernel-trace summary of the default main line.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; O=$R/gpurun_out/r04_final3; mkdir -p "$O"; export TMPDIR=/tmp
