@@ -116,9 +116,6 @@ __device__ __forceinline__ int rg_bvh_classify(float obound, double rbound, doub
     if (!(on <= 1e9) || !(slack <= extent)) return RG_BVH_SCAN;  // also NaN / inf
     double g = 0.0;
     if (slack > 0.25 * margin) {
-#ifdef RG_BVH_DEBUG_NOGROW
-        return RG_BVH_SCAN;
-#endif
         g = slack * (1.0 + 1e-6);
         grow = (float)g;
         if ((double)grow < g) grow = nextafterf(grow, __builtin_huge_valf());

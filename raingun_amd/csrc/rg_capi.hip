@@ -7,8 +7,6 @@
 // abort crosses the ABI.
 #include <hip/hip_runtime.h>
 
-#include <immintrin.h>
-
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -44,9 +42,6 @@ extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStrea
 extern "C" hipError_t rg_render_grid_threads(const RgKernelArgs *a, int maxd, size_t *threads);
 extern "C" int rg_max_array_frames(void);
 extern "C" int rg_launch_global_frames(const RgKernelArgs *a, int maxd);
-#ifndef RG_LIGHT_SINGLE_ORDER
-#define RG_LIGHT_SINGLE_ORDER 0
-#endif
 extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scratch, uint32_t *perm, hipStream_t stream);
 extern "C" size_t rg_tile_order_scratch_words(uint32_t ntiles);
 extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays, uint32_t n, double *dist,
@@ -226,9 +221,6 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
     a.bvh_rbound = s->bvh_rbound;
     a.bvh_margin = s->bvh_margin;
     a.bvh_extent = s->bvh_extent;
-#ifdef RG_BVH_DEBUG_OBOUND  // timing-only ablation builds (unsafe: skips the origin bound)
-    a.bvh_obound = RG_BVH_DEBUG_OBOUND;
-#endif
     a.bodies = s->bodies;
     a.mats = s->mats;
     a.lights = s->lights;
@@ -242,7 +234,7 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
     a.lane_stack = lane ? s->lane_stack : 0;
     a.lane_min_depth = lane ? s->lane_min_depth : 1 << 30;
     // lane_stack entries + one spare slot per lane (rg_kernels.hip bvh_lane, RG_LANE_BRANCHFREE)
-    a.lds_lstack_bytes = lane ? ((uint32_t)(a.lane_stack + 1) * 4u + RG_LANE_HELP_BYTES) * 256u * RG_HEAVY_WPS : 0u;
+    a.lds_lstack_bytes = lane ? ((uint32_t)(a.lane_stack + 1) * 4u) * 256u * RG_HEAVY_WPS : 0u;
     // LDS arena: [lane stacks | sphf | sphf2 | sph | cc (padded to 16 B) | nodes | pln | dsk | box (padded) |
     //             lights | texs (padded) | bodies | mats].  The hot part (staged whenever the sphere
     //             tables are) ends after the texture descriptors: lights and texture descriptors are a
@@ -378,9 +370,9 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     a.prim_sy = cx->prim + width;
     if (!rg_heavy_path(a)) a.lds_blob = lds_blob_for(s, a);  // light path: one staging loop per block
     if (timed && !ok(hipEventRecord(cx->ev0, st))) return RG_ERR_DEVICE;  // kernel_ms includes the tile probe
-    // expensive tiles first: the heavy path always; light single launches when built with
-    // RG_LIGHT_SINGLE_ORDER (persistent waves then start the long ray trees first)
-    if (s->tile_order == 1 || (s->tile_order < 0 && (rg_heavy_path(a) || (RG_LIGHT_SINGLE_ORDER && !pipelined)))) {
+    // expensive tiles first on the heavy path (probe-ordered light tiles measured slower:
+    // DESIGN.md 4g); rg_debug_set_tile_order overrides
+    if (s->tile_order == 1 || (s->tile_order < 0 && rg_heavy_path(a))) {
         const size_t ntiles = (size_t)rg_tile_count(a);
         const rg_launch_ctx::PermKey key{width, height, tiling->tile_rows, tiling->tile_stride, tiling->tile_offset,
                                          tile_first, out_rows, tile_wlog, s->max_depth, (uint32_t)s->n_lights,
@@ -916,39 +908,10 @@ inline void piece(size_t bytes, int i, int n, size_t &off, size_t &len) {
 }
 }  // namespace
 
-#ifndef RG_COPY_NT
-#define RG_COPY_NT 0  // pageable destinations: non-temporal (streaming) stores for the band copies
-#endif
 namespace {
-// A band's copy out of pinned staging into the caller's pageable frame with
-// streaming stores: the destination lines are written whole and not read first
-// (a plain memcpy below glibc's non-temporal threshold reads every destination
-// line for ownership), and they do not evict the staging data from the caches.
-__attribute__((target("avx2"))) void copy_nt_avx2(unsigned char *dst, const unsigned char *src, size_t n) {
-    const size_t head = std::min(n, (size_t)((32u - ((uintptr_t)dst & 31u)) & 31u));
-    std::memcpy(dst, src, head);
-    dst += head;
-    src += head;
-    n -= head;
-    size_t i = 0;
-    for (; i + 128 <= n; i += 128) {
-        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i));
-        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 32));
-        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 64));
-        const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 96));
-        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i), a);
-        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 32), b);
-        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 64), c);
-        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 96), d);
-    }
-    _mm_sfence();
-    std::memcpy(dst + i, src + i, n - i);
-}
-void copy_band(unsigned char *dst, const unsigned char *src, size_t n) {
-    static const bool avx2 = __builtin_cpu_supports("avx2");
-    if (RG_COPY_NT && avx2 && n >= 4096) copy_nt_avx2(dst, src, n);
-    else std::memcpy(dst, src, n);
-}
+// A band's copy out of pinned staging into the caller's pageable frame (non-temporal AVX2 stores
+// measured no consistent change: DESIGN.md 5)
+void copy_band(unsigned char *dst, const unsigned char *src, size_t n) { std::memcpy(dst, src, n); }
 }  // namespace
 
 void rg_copy_pool::run(int id) {

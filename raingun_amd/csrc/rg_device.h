@@ -61,12 +61,6 @@ struct alignas(16) RgBvhNode {
 // lower bound, so pruning at pop is conservative) | the child's node index.
 #define RG_LANE_NODE_BITS 12
 #define RG_LANE_STACK_MAX 16      // entries per lane the LDS arena may hold
-#ifndef RG_LANE_HELP
-#define RG_LANE_HELP 0            // per-lane walk: lanes done with their ray take subtrees of other lanes' rays
-#endif
-// LDS per thread behind the stacks for RG_LANE_HELP: the helpers' closest sphere hit of the
-// thread's ray (u64 key, u32 id code), its occlusion flag and one matching word
-#define RG_LANE_HELP_BYTES (RG_LANE_HELP ? 20u : 0u)
 
 struct RgBodyDev {         // per body, YAML order
     int32_t kind;
@@ -224,9 +218,6 @@ __host__ __device__ inline unsigned long long rg_tile_count(const RgKernelArgs &
 // Kernel path of a launch (the launcher and the host's tile-order policy agree on it).
 __host__ __device__ __forceinline__ bool rg_heavy_path(const RgKernelArgs &a) {
     bool heavy = a.n_sph + a.n_pln + a.n_dsk + a.n_box >= RG_HEAVY_SCENE_BODIES;
-#if defined(RG_FORCE_WPS)
-    heavy = RG_FORCE_WPS != 2;
-#endif
     if (a.path != RG_PATH_AUTO) heavy = a.path == RG_PATH_HEAVY;
     if (a.n_lights > RG_LB) heavy = true;  // the light path shades all lights in ONE batch
     return heavy;

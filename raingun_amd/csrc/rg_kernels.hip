@@ -183,17 +183,7 @@ struct SphLds {
     const RgDsk *dk;
     const RgBox *bx;
     const RgBvhNode *nd;
-#ifndef RG_WAVE_NODE_SCALAR
-#define RG_WAVE_NODE_SCALAR 0
-#endif
-#if RG_WAVE_NODE_SCALAR
-    // the wave-coherent walk's node (wave-uniform index) through scalar loads:
-    // SGPR operands for the box tests instead of 32 broadcast VGPRs
-    const RG_CONST RgBvhNode *nds;
-    __device__ __forceinline__ RgBvhNode getn_uniform(int i) const { return nds[i]; }
-#else
     __device__ __forceinline__ RgBvhNode getn_uniform(int i) const { return nd[i]; }
-#endif
     __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
     __device__ __forceinline__ RgSph getv(int i) const { return s[i]; }
     __device__ __forceinline__ RgPln getp(int i) const { return pl[i]; }
@@ -254,15 +244,8 @@ __device__ __forceinline__ bool filter_primary(const RgSphF &f, const RgSphF2 &f
     return !(opp > f2.thrp);
 }
 
-#ifndef RG_SPHERE_UV_NOINLINE
-#define RG_SPHERE_UV_NOINLINE 1
-#endif
-#ifndef RG_SPH_GROUP
 #define RG_SPH_GROUP 2     // spheres per exact miss-test group (one divergent branch per group)
-#endif
-#ifndef RG_FILTER_GROUP
-#define RG_FILTER_GROUP 4  // spheres per f32-filter group
-#endif
+#define RG_FILTER_GROUP 4  // spheres per f32-filter group (2 and 8 measured slower)
 
 // Primary rays start at the origin (ray.rs:53): h = c - 0 = c exactly, so
 // h.h = c.c is a per-sphere constant (bit-identical): 8 FP64 ops per sphere.
@@ -481,42 +464,15 @@ __device__ __forceinline__ void leaf_primary(const RgKernelArgs &a, const Src &s
     }
 }
 
-#ifndef RG_LEAF_PREFETCH
-#define RG_LEAF_PREFETCH 0  // BVH leaf tests on global sphere tables: the next sphere's filter records read ahead
-#endif
 template <class Src>
 __device__ __forceinline__ void leaf_query(const RgKernelArgs &a, const Src &src, int first, int count, V3 o, V3 d,
                                            const RayF &rf, bool shadow, double ld, Closest &c, bool &occl,
                                            bool &need) {
-    // RG_LEAF_PREFETCH, sphere tables in global memory (scenes too large for LDS): the next
-    // sphere's filter records are read before this sphere's tests, so their round trip overlaps
-    // the filter and the exact test.  Off: the configs[4] line at 16384^2 is unchanged (206.28
-    // vs 206.30 ms; 5-frame 1080p samples -3..-6 %, within their noise); from LDS the extra
-    // registers cost more than the overlap saves (north star 2.448 -> 2.532 ms, 6 -> 13
-    // spilled VGPRs; profiles/r04/s24, s25)
-    constexpr bool PF = RG_LEAF_PREFETCH && !Src::in_lds;
-    RgSphF fn;
-    RgSphF2 f2n;
-    if constexpr (PF) {
-        fn = src.getf(first);
-        f2n = src.getf2(first);
-    }
     for (int j = first; j < first + count; ++j) {
         // the id comes with the filter record (RgSphF2::id): a per-lane j (bvh_lane) would
         // otherwise make sph_id[j] a vector global load whose latency the hit waits for
-        RgSphF f;
-        RgSphF2 f2;
-        if constexpr (PF) {
-            f = fn;
-            f2 = f2n;
-            if (j + 1 < first + count) {
-                fn = src.getf(j + 1);
-                f2n = src.getf2(j + 1);
-            }
-        } else {
-            f = src.getf(j);
-            f2 = src.getf2(j);
-        }
+        const RgSphF f = src.getf(j);
+        const RgSphF2 f2 = src.getf2(j);
         if (need && filter_general(f, f2, rf)) {
             const RgSph s = src.get(j);
             const double hx = s.cx - o.x, hy = s.cy - o.y, hz = s.cz - o.z;
@@ -636,118 +592,24 @@ __device__ __forceinline__ void cswap(uint32_t &x, uint32_t &y) {
     y = hi;
 }
 
-#ifndef RG_LANE_BRANCHFREE
-#define RG_LANE_BRANCHFREE 1  // per-lane walk: child slots processed without divergent branches (one spare stack slot)
-#endif
-#ifndef RG_LANE_TOP
-#define RG_LANE_TOP 0  // per-lane walk: the stack's top entry in a register (pops without an LDS read;
-                       // north star 2.4387 -> 2.4307 ms over 60 frames, 20 frames equal: within noise, off)
-#endif
-#ifndef RG_LANE_CLOCK_WORD
-#define RG_LANE_CLOCK_WORD 12  // RG_BVH_STATS: counter word of the per-lane walk's clock (13: apart from the wave walk's)
-#endif
-#ifndef RG_LANE_LEAF_BATCH
-#define RG_LANE_LEAF_BATCH 0  // 1: the per-lane walk postpones leaf tests and runs them in batches (below)
-#endif
-
 template <class Src>
 __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, V3 o, V3 d, bool shadow, double ld,
                                          double t0s, Closest &c, bool &occl, bool &need) {
     uint32_t *stk = reinterpret_cast<uint32_t *>(rg_dyn_smem) + threadIdx.x;  // entry e at stk[e * blockDim.x]
     const uint32_t stride = blockDim.x;
-    const int cap = a.lane_stack;
     const uint32_t mask = (1u << RG_LANE_NODE_BITS) - 1u;
     const V3 ob = t0s > 0.0 ? add(o, scl(d, t0s)) : o;
     const RayB rb = rg_make_rayb(ob.x, ob.y, ob.z, d.x, d.y, d.z);
     const RayF rf = make_rayf(o, d);
     const float tld = shadow ? bvh_bound(ld - t0s) : 0.0f;
     int node = 0;
-    [[maybe_unused]] int sp = 0;
     RG_STAT(4, 1);
     RG_STAT(7, RG_LANES(1));
     [[maybe_unused]] const unsigned long long t_in = RG_CLOCK();
-#if RG_LANE_LEAF_BATCH
-    // Speculative traversal (Aila & Laine 2009): a lane keeps the leaves a node
-    // visit finds pending and visits no further node until they are tested; the
-    // wave tests leaves only when at least as many lanes hold one as could visit
-    // a node (or none can), so a leaf round runs with many lanes instead of the
-    // few whose node happened to have leaf children.  Leaf tests commute
-    // (closest_add, any-hit), and pruning with a bound not yet tightened by the
-    // postponed leaves only culls less: results are identical.
-    int l0 = 0, l1 = 0, l2 = 0, l3 = 0, nl = 0;
-    for (;;) {
-        const bool visit = need && node >= 0 && nl == 0;
-        const bool leaf = need && nl > 0;
-        const int nv = __builtin_popcountll(__ballot(visit)), nlf = __builtin_popcountll(__ballot(leaf));
-        if (nv + nlf == 0) break;
-        RG_STAT(5, 1);
-#ifdef RG_ITER_STATS
-        {
-            if ((int)(threadIdx.x & 63u) == __builtin_ffsll((long long)__ballot(1)) - 1) {
-                atomicAdd(&a.counters[nlf >= nv ? 14 : 12], 1ull);
-                atomicAdd(&a.counters[nlf >= nv ? 15 : 13], (unsigned long long)(nlf >= nv ? nlf : nv));
-            }
-        }
-#endif
-        if (nlf >= nv) {  // leaf round: every lane holding a leaf tests one
-            if (leaf) {
-                const int v = ~l0;
-                leaf_query(a, src, v >> 3, (v & 7) + 1, o, d, rf, shadow, ld, c, occl, need);
-                l0 = l1; l1 = l2; l2 = l3;
-                --nl;
-            }
-            continue;
-        }
-        if (visit) {
-            const RgBvhNode N = src.getn(node);
-            const float tb = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
-            uint32_t e0 = ~0u, e1 = ~0u, e2 = ~0u, e3 = ~0u;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                float tn = 0.0f;
-                if (k < N.nchild && rg_child_hit(N, k, rb, tb, tn)) {
-                    const int ch = N.child[k];
-                    if (ch < 0) {
-                        if (nl == 0) l0 = ch;
-                        else if (nl == 1) l1 = ch;
-                        else if (nl == 2) l2 = ch;
-                        else l3 = ch;
-                        ++nl;
-                    } else {
-                        const uint32_t e = lane_key(tn, ch);
-                        if (k == 0) e0 = e;
-                        else if (k == 1) e1 = e;
-                        else if (k == 2) e2 = e;
-                        else e3 = e;
-                    }
-                }
-            }
-            cswap(e0, e1); cswap(e2, e3); cswap(e0, e2); cswap(e1, e3); cswap(e1, e2);
-            if (e3 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e3;
-            if (e2 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e2;
-            if (e1 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e1;
-            if (e0 != ~0u && (shadow || !(lane_key_t(e0) > tb))) {
-                node = (int)(e0 & mask);
-            } else {
-                node = -1;
-                while (sp > 0) {
-                    const uint32_t e = stk[(uint32_t)(--sp) * stride];
-                    if (shadow || !(lane_key_t(e) > tb)) {
-                        node = (int)(e & mask);
-                        break;
-                    }
-                }
-            }
-        }
-    }
-#else
-#if RG_LANE_BRANCHFREE
-    const uint32_t capo = (uint32_t)cap * stride;
+    // slot `cap` is a spare: a write that is not a push may land there, never on an entry;
+    // the stack pointer is kept scaled by the stride (spo = sp * stride: no multiplies)
+    const uint32_t capo = (uint32_t)a.lane_stack * stride;
     uint32_t spo = 0u;
-#if RG_LANE_TOP
-    uint32_t top = ~0u;  // the stack's top entry, in a register (~0: none)
-#endif
-#endif
     for (;;) {
         const bool act = need && node >= 0;
         if (!__any(act)) break;
@@ -761,7 +623,6 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             }
         }
 #endif
-#if RG_LANE_BRANCHFREE
         if (act) {
             // the node's children without divergent branches: every slot's slab test,
             // hit leaves as a bit mask (tested below in child order), hit internal
@@ -787,51 +648,17 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             uint32_t e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
             // ascending (entry distance, node); empty slots (~0) last
             cswap(e0, e1); cswap(e2, e3); cswap(e0, e2); cswap(e1, e3); cswap(e1, e2);
-            // slot `cap` is a spare: a write that is not a push may land there, never on an entry;
-            // the stack pointer is kept scaled by the stride (spo = sp * stride: no multiplies)
-#if RG_LANE_TOP
-            // the stack's top entry stays in a register (`top`): the entry a node visit pushes
-            // last (e1) is the one the walk most often pops next, without an LDS round trip;
-            // the previous top goes to LDS under the new pushes (LIFO order unchanged)
-            const bool p1 = e1 != ~0u;  // sorted: e2, e3 are empty when e1 is
-            stk[min(spo, capo)] = top;
-            spo += (p1 & (top != ~0u) & (spo < capo)) ? stride : 0u;
-            stk[min(spo, capo)] = e3;
-            spo += ((e3 != ~0u) & (spo < capo)) ? stride : 0u;
-            stk[min(spo, capo)] = e2;
-            spo += ((e2 != ~0u) & (spo < capo)) ? stride : 0u;
-            top = p1 ? e1 : top;
-#else
             stk[min(spo, capo)] = e3;
             spo += ((e3 != ~0u) & (spo < capo)) ? stride : 0u;
             stk[min(spo, capo)] = e2;
             spo += ((e2 != ~0u) & (spo < capo)) ? stride : 0u;
             stk[min(spo, capo)] = e1;
             spo += ((e1 != ~0u) & (spo < capo)) ? stride : 0u;
-#endif
             const float tbn = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
             if (e0 != ~0u && (shadow || !(lane_key_t(e0) > tbn))) {
                 node = (int)(e0 & mask);
             } else {
                 node = -1;
-#if RG_LANE_TOP
-                while (need) {
-                    uint32_t e;
-                    if (top != ~0u) {
-                        e = top;
-                        top = ~0u;
-                    } else if (spo > 0u) {
-                        spo -= stride;
-                        e = stk[spo];
-                    } else {
-                        break;
-                    }
-                    if (shadow || !(lane_key_t(e) > tbn)) {
-                        node = (int)(e & mask);
-                        break;
-                    }
-                }
-#else
                 while (spo > 0u && need) {
                     spo -= stride;
                     const uint32_t e = stk[spo];
@@ -840,326 +667,11 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
                         break;
                     }
                 }
-#endif
-            }
-        }
-#else
-        if (act) {
-            const RgBvhNode N = src.getn(node);
-            const float tb = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
-            uint32_t e0 = ~0u, e1 = ~0u, e2 = ~0u, e3 = ~0u;
-            int l0 = 0, l1 = 0, l2 = 0, l3 = 0, nl = 0;  // hit leaf children, in child order
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                float tn = 0.0f;
-                if (k < N.nchild && need && rg_child_hit(N, k, rb, tb, tn)) {
-                    const int ch = N.child[k];
-                    if (ch < 0) {
-                        if (nl == 0) l0 = ch;
-                        else if (nl == 1) l1 = ch;
-                        else if (nl == 2) l2 = ch;
-                        else l3 = ch;
-                        ++nl;
-                    } else {
-                        const uint32_t e = lane_key(tn, ch);
-                        if (k == 0) e0 = e;
-                        else if (k == 1) e1 = e;
-                        else if (k == 2) e2 = e;
-                        else e3 = e;
-                    }
-                }
-            }
-            // leaves first (they tighten a closest-hit bound): ONE copy of the leaf
-            // test, looped max-over-lanes times, instead of one per child slot
-            while (nl > 0 && need) {
-#ifdef RG_ITER_STATS  // leaf-test iterations, lanes testing a leaf (counters[14..15])
-                {
-                    const unsigned long long m = __ballot(1);
-                    if ((int)(threadIdx.x & 63u) == __builtin_ffsll((long long)m) - 1) {
-                        atomicAdd(&a.counters[14], 1ull);
-                        atomicAdd(&a.counters[15], (unsigned long long)__builtin_popcountll(m));
-                    }
-                }
-#endif
-                const int v = ~l0;
-                leaf_query(a, src, v >> 3, (v & 7) + 1, o, d, rf, shadow, ld, c, occl, need);
-                l0 = l1; l1 = l2; l2 = l3;
-                --nl;
-            }
-            // ascending (entry distance, node); empty slots (~0) last
-            cswap(e0, e1); cswap(e2, e3); cswap(e0, e2); cswap(e1, e3); cswap(e1, e2);
-            if (e3 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e3;
-            if (e2 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e2;
-            if (e1 != ~0u && sp < cap) stk[(uint32_t)(sp++) * stride] = e1;
-            const float tbn = shadow ? tld : (c.id >= 0 ? bvh_bound(c.t - t0s) : __builtin_huge_valf());
-            if (e0 != ~0u && (shadow || !(lane_key_t(e0) > tbn))) {
-                node = (int)(e0 & mask);
-            } else {
-                node = -1;
-                while (sp > 0 && need) {
-                    const uint32_t e = stk[(uint32_t)(--sp) * stride];
-                    if (shadow || !(lane_key_t(e) > tbn)) {
-                        node = (int)(e & mask);
-                        break;
-                    }
-                }
-            }
-        }
-#endif
-    }
-#endif
-    RG_STAT(RG_LANE_CLOCK_WORD, RG_CLOCK() - t_in);
-}
-
-#if RG_LANE_HELP
-// Per-lane walk with helpers (RG_LANE_HELP).  The lanes of a wave finish their
-// walks at different times; in bvh_lane the finished ones idle until the
-// wave's longest walk is done (25 of 64 lanes active per iteration on the
-// north star).  Here, whenever few lanes are still walking, a balancing step
-// lets every idle lane -- done with its ray, or never given one -- take the
-// BOTTOM entry of a walking lane's stack (the shallowest deferred subtree) and
-// walk that subtree for the walking lane's ray: the ray (o, d, light distance,
-// start offset, current closest hit as the bound) comes over ds_bpermute, the
-// subtree is walked with the helper's own stack.  A helper's finds go to the
-// ray's result slot in LDS: closest sphere hit as an atomic min over (key =
-// t's bits without the sign, then code = id << 1 | sign bit), occlusion as a
-// flag; walking lanes fold their ray's slot into their bound at every step.
-// The accepted set is what bvh_lane accepts (same boxes and leaf tests; a
-// subtree skipped only when its entry distance exceeds a bound that is a
-// closest hit the ray really has), and the closest-hit rule is an
-// order-independent lexicographic minimum, so the result is identical.
-#ifndef RG_HELP_ACTIVE
-#define RG_HELP_ACTIVE 40  // a balancing step runs when at most this many lanes walk ...
-#endif
-#ifndef RG_HELP_MIN_IDLE
-#define RG_HELP_MIN_IDLE 8  // ... at least this many could help, and some walking lane has a deferred subtree
-#endif
-#ifndef RG_HELP_ROUNDS
-#define RG_HELP_ROUNDS 1  // matching rounds per balancing step
-#endif
-// The slots are read by other lanes than the ones that wrote them: relaxed atomics on
-// different addresses may be reordered by the compiler, so a step's writes and the next
-// step's reads are separated by a fence (one wave: LDS executes its operations in order)
-__device__ __forceinline__ void help_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
-__device__ __forceinline__ unsigned long long help_ld64(unsigned long long *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
-__device__ __forceinline__ uint32_t help_ld32(uint32_t *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
-__device__ __forceinline__ void help_st64(unsigned long long *p, unsigned long long v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
-__device__ __forceinline__ void help_st32(uint32_t *p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
-__device__ __forceinline__ uint32_t help_pull(int src_lane, uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
-}
-__device__ __forceinline__ double help_pull_d(int src_lane, double v) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const uint32_t lo = help_pull(src_lane, (uint32_t)b), hi = help_pull(src_lane, (uint32_t)(b >> 32));
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-// closest-hit rule (closest_add without the count) on (t, id)
-__device__ __forceinline__ void help_fold(double &ct, int &cid, double t, int id) {
-    if (id >= 0 && (cid < 0 || t < ct || (t == ct && id < cid))) { ct = t; cid = id; }
-}
-
-template <class Src>
-__device__ __forceinline__ void bvh_lane_help(const RgKernelArgs &a, const Src &src, const V3 o_in, const V3 d_in,
-                                              bool shadow_in, double ld_in, double t0s_in, Closest &c_in,
-                                              bool &occl_in, bool &need_in, bool mine) {
-    const uint32_t stride = blockDim.x;
-    uint32_t *stk = reinterpret_cast<uint32_t *>(rg_dyn_smem) + threadIdx.x;  // entry e at stk[e * stride]
-    const uint32_t capo = (uint32_t)a.lane_stack * stride;
-    const uint32_t mask = (1u << RG_LANE_NODE_BITS) - 1u;
-    const int lane = (int)(threadIdx.x & 63u);
-    const uint32_t wbase = threadIdx.x & ~63u;
-    // behind the stacks (+ spare slot): u64 keys, u32 id codes, u32 flags, u32 matching words
-    unsigned long long *slot_t =
-        reinterpret_cast<unsigned long long *>(rg_dyn_smem + (size_t)(a.lane_stack + 1) * stride * 4u) + wbase;
-    uint32_t *slot_i = reinterpret_cast<uint32_t *>(slot_t - wbase + stride) + wbase;
-    uint32_t *slot_o = slot_i + stride;
-    uint32_t *match = slot_o + stride;
-    help_st64(&slot_t[lane], ~0ull);
-    help_st32(&slot_i[lane], ~0u);
-    help_st32(&slot_o[lane], 0u);
-    const int nexec = __builtin_popcountll(__ballot(1));
-
-    // the lane's current walk (its own ray, or a subtree of another lane's ray for `owner`)
-    V3 o = o_in, d = d_in;
-    bool shadow = shadow_in;
-    double ld = ld_in, t0s = t0s_in;
-    double ct = c_in.t;
-    int cid = c_in.id;
-    bool need = mine && need_in, occl = false;
-    bool open = need;
-    int owner = lane;
-    RayB rb;
-    RayF rf;
-    float tld;
-    auto setup = [&]() {
-        const V3 ob = t0s > 0.0 ? add(o, scl(d, t0s)) : o;
-        rb = rg_make_rayb(ob.x, ob.y, ob.z, d.x, d.y, d.z);
-        rf = make_rayf(o, d);
-        tld = shadow ? bvh_bound(ld - t0s) : 0.0f;
-    };
-    setup();
-    int node = 0;
-    uint32_t spo = 0u, boto = 0u;  // stack [boto, spo), scaled by the stride
-    RG_STAT(4, 1);
-    RG_STAT(7, RG_LANES(need));
-    [[maybe_unused]] const unsigned long long t_in = RG_CLOCK();
-    for (;;) {
-        const bool act = open && need && node >= 0;
-        const int nact = __builtin_popcountll(__ballot(act));
-        const bool donor = act && spo > boto;
-        const unsigned long long dm = __ballot(donor);
-        if (nact == 0 || (nact <= RG_HELP_ACTIVE && nexec - nact >= RG_HELP_MIN_IDLE && dm != 0ull)) {
-            // ---- balancing step (wave-uniform)
-            // 1. retire finished walks into their ray's slot (atomic min on the key; the id code
-            //    is reset when the key drops).  Every hit distance is >= 0 or -0 (bodies.rs
-            //    tests), so the key orders them as doubles do.
-            const bool fin = open && !act;
-            const bool put = fin && !shadow && cid >= 0 && !(ct < 0.0);
-            const unsigned long long key = (unsigned long long)__double_as_longlong(ct) & 0x7FFFFFFFFFFFFFFFull;
-            const uint32_t code = ((uint32_t)cid << 1) | (uint32_t)(__double_as_longlong(ct) < 0);
-            if (fin && occl) help_st32(&slot_o[owner], 1u);
-            unsigned long long told = 0ull;
-            if (put) told = help_ld64(&slot_t[owner]);
-            if (put) atomicMin(&slot_t[owner], key);
-            unsigned long long tnew = 0ull;
-            if (put) tnew = help_ld64(&slot_t[owner]);
-            if (put && key == tnew && tnew < told) help_st32(&slot_i[owner], ~0u);
-            if (put && key == tnew) atomicMin(&slot_i[owner], code);
-            help_fence();  // the slots' updates by every lane before any lane reads them
-            if (fin) open = false;
-            if (nact == 0) break;
-            // 2. walking lanes fold their ray's slot into their bound (a shadow ray another lane
-            //    found occluded stops)
-            if (open) {
-                if (shadow) {
-                    if (help_ld32(&slot_o[owner]) != 0u) { occl = true; need = false; }
-                } else {
-                    const unsigned long long st = help_ld64(&slot_t[owner]);
-                    if (st != ~0ull) {
-                        const uint32_t sc = help_ld32(&slot_i[owner]);
-                        help_fold(ct, cid, __longlong_as_double((long long)(st | ((unsigned long long)(sc & 1u) << 63))),
-                                  (int)(sc >> 1));
-                    }
-                }
-            }
-            // 3. idle lane of rank i takes the bottom stack entry of the walking lane of rank i
-            //    (RG_HELP_ROUNDS times: a lone ray's deferred subtrees go to several helpers)
-            for (int round = 0; round < RG_HELP_ROUNDS; ++round) {
-                const bool idle = !open;
-                const bool don = open && need && node >= 0 && spo > boto;
-                const unsigned long long im = __ballot(idle), dm2 = __ballot(don);
-                const int k = min(__builtin_popcountll(im), __builtin_popcountll(dm2));
-                if (k == 0) break;
-                const int ri = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
-                const int rd = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(dm2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm2, 0u));
-                const bool robbed = don && rd < k, steal = idle && ri < k;
-                if (robbed) help_st32(&match[rd], (uint32_t)lane);
-                help_fence();
-                int dl = lane;
-                if (steal) dl = (int)help_ld32(&match[ri]);
-                const uint32_t bent = stk[min(boto, capo)];
-                const uint32_t e = help_pull(dl, bent);
-                const V3 no = v3(help_pull_d(dl, o.x), help_pull_d(dl, o.y), help_pull_d(dl, o.z));
-                const V3 nd = v3(help_pull_d(dl, d.x), help_pull_d(dl, d.y), help_pull_d(dl, d.z));
-                const double nld = help_pull_d(dl, ld), nt0s = help_pull_d(dl, t0s), nct = help_pull_d(dl, ct);
-                const int ncid = (int)help_pull(dl, (uint32_t)cid);
-                const uint32_t nos = help_pull(dl, (uint32_t)owner | (shadow ? 0x100u : 0u));
-                if (robbed) boto += stride;
-                if (steal) {
-                    o = no;
-                    d = nd;
-                    ld = nld;
-                    t0s = nt0s;
-                    ct = nct;
-                    cid = ncid;
-                    owner = (int)(nos & 0xFFu);
-                    shadow = (nos & 0x100u) != 0u;
-                    occl = false;
-                    need = true;
-                    open = true;
-                    spo = 0u;
-                    boto = 0u;
-                    setup();
-                    const float tb = shadow ? tld : (cid >= 0 ? bvh_bound(ct - t0s) : __builtin_huge_valf());
-                    node = (shadow || !(lane_key_t(e) > tb)) ? (int)(e & mask) : -1;
-                }
-            }
-        }
-        if (!(open && need && node >= 0)) continue;
-        RG_STAT(5, 1);
-#ifdef RG_ITER_STATS  // per-lane walk: iterations, active lanes (counters[12..13])
-        {
-            const unsigned long long m = __ballot(1);
-            if ((int)(threadIdx.x & 63u) == __builtin_ffsll((long long)m) - 1) {
-                atomicAdd(&a.counters[12], 1ull);
-                atomicAdd(&a.counters[13], (unsigned long long)__builtin_popcountll(m));
-            }
-        }
-#endif
-        // one node (bvh_lane, RG_LANE_BRANCHFREE)
-        const RgBvhNode N = src.getn(node);
-        const float tb = shadow ? tld : (cid >= 0 ? bvh_bound(ct - t0s) : __builtin_huge_valf());
-        uint32_t e[4], leaves = 0u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float tn = 0.0f;
-            const bool h = (k < N.nchild) & rg_child_hit(N, k, rb, tb, tn);
-            const int ch = N.child[k];
-            leaves |= (h & (ch < 0)) ? (1u << k) : 0u;
-            e[k] = (h & (ch >= 0)) ? lane_key(tn, ch) : ~0u;
-        }
-        Closest c;
-        c.t = ct;
-        c.id = cid;
-        c.nhit = 0;
-        c.nan = false;
-        while (leaves != 0u && need) {
-            const uint32_t k = (uint32_t)__builtin_ctz(leaves);
-            leaves &= leaves - 1u;
-            const int v = ~(k == 0u ? N.child[0] : k == 1u ? N.child[1] : k == 2u ? N.child[2] : N.child[3]);
-            leaf_query(a, src, v >> 3, (v & 7) + 1, o, d, rf, shadow, ld, c, occl, need);
-        }
-        ct = c.t;
-        cid = c.id;
-        uint32_t e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
-        cswap(e0, e1); cswap(e2, e3); cswap(e0, e2); cswap(e1, e3); cswap(e1, e2);
-        stk[min(spo, capo)] = e3;
-        spo += ((e3 != ~0u) & (spo < capo)) ? stride : 0u;
-        stk[min(spo, capo)] = e2;
-        spo += ((e2 != ~0u) & (spo < capo)) ? stride : 0u;
-        stk[min(spo, capo)] = e1;
-        spo += ((e1 != ~0u) & (spo < capo)) ? stride : 0u;
-        const float tbn = shadow ? tld : (cid >= 0 ? bvh_bound(ct - t0s) : __builtin_huge_valf());
-        if (e0 != ~0u && (shadow || !(lane_key_t(e0) > tbn))) {
-            node = (int)(e0 & mask);
-        } else {
-            node = -1;
-            while (spo > boto && need) {
-                spo -= stride;
-                const uint32_t en = stk[spo];
-                if (shadow || !(lane_key_t(en) > tbn)) {
-                    node = (int)(en & mask);
-                    break;
-                }
             }
         }
     }
-    help_fence();
-    if (mine) {  // what the own walk and the helpers found for this ray
-        const unsigned long long st = help_ld64(&slot_t[lane]);
-        if (st != ~0ull) {
-            const uint32_t sc = help_ld32(&slot_i[lane]);
-            c_in.t = __longlong_as_double((long long)(st | ((unsigned long long)(sc & 1u) << 63)));
-            c_in.id = (int)(sc >> 1);
-        }
-        if (help_ld32(&slot_o[lane]) != 0u) {
-            occl_in = true;
-            need_in = false;
-        }
-    }
-    RG_STAT(RG_LANE_CLOCK_WORD, RG_CLOCK() - t_in);
+    RG_STAT(12, RG_CLOCK() - t_in);
 }
-#endif
 
 template <bool F32F, bool BVH, class Src>
 __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
@@ -1280,23 +792,10 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
             RG_STAT(13, RG_CLOCK() - t0);
         }
         const bool grown = ok && grow > 0.0f;  // far rays: boxes grown in the slab test
-#ifndef RG_MIX_LANE
-#define RG_MIX_LANE 1
-#endif
-#if RG_MIX_LANE
         // one walk kind per wave: if any lane's ray is incoherent, every near lane walks per lane
         // (a mixed wave would otherwise run the per-lane walk and then the wave walk)
         const bool per_lane = ok && !grown && a.lane_stack > 0 && __any(ok && !grown && lane_walk);
-#else
-        const bool per_lane = ok && !grown && lane_walk && a.lane_stack > 0;  // incoherent rays
-#endif
-#if RG_LANE_HELP
-        if (__any(per_lane)) bvh_lane_help(a, src, o, d, shadow, ld, t0s, c, occl, need, per_lane);
-#else
-        if (per_lane) {
-            bvh_lane(a, src, o, d, shadow, ld, t0s, c, occl, need);
-        }
-#endif
+        if (per_lane) bvh_lane(a, src, o, d, shadow, ld, t0s, c, occl, need);
         if (ok && !grown && !per_lane) {
             bvh_spheres<1>(a, src, o, d, shadow, ld, t0s, c, occl, need);
         }
@@ -1327,9 +826,6 @@ __device__ __forceinline__ bool ray_exotic(V3 o, V3 d) {
 // 8 + 3*8 FP64 ops per sphere instead of 3*16, with bit-identical per-ray
 // arithmetic.  Bit l of `occl` = light l of the batch is occluded.
 // RG_LB (lights per shadow batch on the light path) lives in rg_device.h
-#ifndef RG_LIGHT_SHADOW_FILTER
-#define RG_LIGHT_SHADOW_FILTER 0  // light path: f32 pre-filter in the shadow batches only
-#endif
 #ifndef RG_SHADOW_GROUP
 #define RG_SHADOW_GROUP 2  // spheres per miss-test group in the shadow pass
 #endif
@@ -1340,57 +836,13 @@ struct ShadowBatch {
     double ld[LB];      // light.distance(hit) (lights.rs:53-58), +inf for directional
 };
 
-// F32F: the f32 pre-filter (above) in front of each group's exact tests: a group
-// runs the reference's f64 arithmetic only when some lane and light of the wave
-// may hit one of its spheres.  The batch's directions are unit vectors
-// (direction_from normalizes, lights.rs:46-51), so Kd is one constant (|d|^2 <=
-// 1.0001, checked per batch: a wave with another direction keeps the exact
-// tests only), and the threshold of a sphere is light-independent.
-template <int LB, bool F32F = false, class Src>
+template <int LB, class Src>
 __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &src, V3 o, const ShadowBatch<LB> &sb,
                                              uint32_t full, uint32_t &occl) {
     constexpr int G = RG_SHADOW_GROUP;
     const int n = a.n_sph, nfull = n - n % G;
-    [[maybe_unused]] constexpr float KD1 = 5.9604645e-08f * (16.2f + 26.2f * 1.0001f) * 1.01f;
-    [[maybe_unused]] bool filt = false;
-    [[maybe_unused]] float ox = 0.0f, oy = 0.0f, oz = 0.0f, kdo2 = 0.0f, fdx[LB], fdy[LB], fdz[LB];
-    if constexpr (F32F) {
-        bool unit = true;
-#pragma unroll
-        for (int l = 0; l < LB; ++l) {
-            unit &= dot(sb.d[l], sb.d[l]) <= 1.0001;  // NaN: false (exact tests only)
-            fdx[l] = (float)sb.d[l].x; fdy[l] = (float)sb.d[l].y; fdz[l] = (float)sb.d[l].z;
-        }
-        filt = !__any(!unit);
-        ox = (float)o.x; oy = (float)o.y; oz = (float)o.z;
-        kdo2 = KD1 * ((float)dot(o, o) * 1.000001f) * 1.000001f;  // >= Kd |o|^2 (make_rayf)
-    }
     for (int i = 0; i < n;) {
         const int g = i < nfull ? G : 1;  // wave-uniform
-        if constexpr (F32F) {
-            if (filt) {
-                bool cand = false;
-#pragma unroll
-                for (int k = 0; k < G; ++k) {
-                    if (k < g) {
-                        const RgSphF f = src.getf(i + k);
-                        const float hx = f.cx - ox, hy = f.cy - oy, hz = f.cz - oz;
-                        const float hh = __builtin_fmaf(hz, hz, __builtin_fmaf(hy, hy, hx * hx));
-                        const float thr = __builtin_fmaf(KD1, src.getf2(i + k).cchi, f.r2hi + kdo2);
-#pragma unroll
-                        for (int l = 0; l < LB; ++l) {
-                            const float adj = __builtin_fmaf(hz, fdz[l], __builtin_fmaf(hy, fdy[l], hx * fdx[l]));
-                            cand |= !(__builtin_fmaf(-adj, adj, hh) > thr) && !((occl >> l) & 1u);
-                        }
-                    }
-                }
-                if (!__any(cand)) {  // every lane and light of the wave certainly misses the group
-                    i += g;
-                    if ((i & 7) == 0 && !__any(occl != full)) return;
-                    continue;
-                }
-            }
-        }
         RgSph s[G];
         double hx[G], hy[G], hz[G], hh[G], adj[G][LB], opp[G][LB];
         bool cand[G][LB];
@@ -1488,11 +940,7 @@ __device__ __forceinline__ bool surface_normal(const RgBodyDev &b, V3 h, V3 &n) 
 // Sphere texture coordinates (bodies.rs:126-132).  Kept out of line: the
 // f64 atan2/acos expansions need ~70 VGPRs, and inlined into the megakernel
 // they set its register peak (247 VGPRs) while every other live value waits.
-#if RG_SPHERE_UV_NOINLINE
 __device__ __attribute__((noinline))
-#else
-__device__ __forceinline__
-#endif
 float2 sphere_uv(double hx, double hy, double hz, double r) {  // returned in VGPRs (no scratch round trip)
     return make_float2((1.0f + ((float)atan2(hz, hx)) / PI_F) * 0.5f, ((float)acos(hy / r)) / PI_F);
 }
@@ -1501,9 +949,6 @@ float2 sphere_uv(double hx, double hy, double hz, double r) {  // returned in VG
 __device__ __forceinline__ void texture_coords(const RgBodyDev &b, V3 h, float &tx, float &ty) {
     if (b.kind == RG_BODY_SPHERE) {
         V3 hv = sub(h, bp3(b, 0));
-#ifdef RG_DBG_NO_ATAN  // timing ablation only (wrong images)
-        tx = (float)hv.x; ty = (float)hv.y; return;
-#endif
         const float2 uv = sphere_uv(hv.x, hv.y, hv.z, b.p[3]);
         tx = uv.x;
         ty = uv.y;
@@ -1539,9 +984,6 @@ __device__ __forceinline__ float u8_div255(uint32_t b) {
 
 __device__ __forceinline__ C3 material_color(const RgTexDev *texs, const RgMatDev &m, float tx, float ty) {
     if (m.coloration == RG_COLORATION_COLOR) return c3(m.color[0], m.color[1], m.color[2]);
-#ifdef RG_DBG_NO_TEX  // timing ablation only (wrong images)
-    return c3(0.5f, 0.5f, 0.5f);
-#endif
     const RgTexDev t = texs[m.tex];
     uint32_t x = wrap(tx + m.xoff, t.w);
     uint32_t y = wrap(ty + m.yoff, t.h);
@@ -1551,7 +993,7 @@ __device__ __forceinline__ C3 material_color(const RgTexDev *texs, const RgMatDe
     return c3(u8_div255(px & 0xffu), u8_div255((px >> 8) & 0xffu), u8_div255((px >> 16) & 0xffu));
 }
 
-// material_color in two halves (light path, RG_LIGHT_TEXEL_EARLY): the texel load
+// material_color in two halves (light path): the texel load
 // is issued at the hit and its conversion runs after the shadow batch's setup, so
 // the load's latency overlaps the per-light work instead of stalling the wave.
 __device__ __forceinline__ uint32_t texel_fetch(const RgTexDev *texs, const RgMatDev &m, const RgBodyDev &b, V3 h) {
@@ -1782,26 +1224,21 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 // refractive pixels (the slowest tiles, which bound a frame's makespan)
 // across the waves of a CU.  Waits only ever point down a tree, so there is
 // no cycle: every awaited subtree is held by a live lane.
+#ifndef RG_PIPE_TILES_PER_WAVE
+#define RG_PIPE_TILES_PER_WAVE 32  // heavy launches with frames in flight (launch_one, RgKernelArgs::pipelined)
+#endif
+#ifndef RG_PIPE_MIN_CU_DIV
+#define RG_PIPE_MIN_CU_DIV 4  // ... and at least 1/this of the CUs' blocks (3 -> 4: north-star 1/8 share 0.349 -> 0.327 ms)
+#endif
 // Light path, non-persistent waves: a wave renders at most this many 8x8 tiles
 // and exits, and the grid holds one wave per that many tiles, so the hardware
 // dispatcher hands out CU slots wave by wave -- across the kernels of frames in
 // flight too -- instead of 3072 persistent waves pinning their slots until the
-// frame's queue is empty.  0 = persistent.  16 measured best for the whole 4K
-// frame and for 1/2 .. 1/8 shares (profiles/r01/variants_light_tiles_per_wave.txt).
-#ifndef RG_PIPE_MIN_CU_DIV
-#define RG_PIPE_MIN_CU_DIV 4  // ... and at least 1/this of the CUs' blocks (3 -> 4: north-star 1/8 share 0.349 -> 0.327 ms)
-#endif
-#ifndef RG_PIPE_TILES_PER_WAVE
-#define RG_PIPE_TILES_PER_WAVE 32  // heavy launches with frames in flight (launch_one, RgKernelArgs::pipelined)
-#endif
+// frame's queue is empty.  16 measured best for the whole 4K frame and for
+// 1/2 .. 1/8 shares (profiles/r01/variants_light_tiles_per_wave.txt; 12 / 20 / 32
+// re-measured in rounds 3-4: profiles/r04/s29, profiles/r04/s13).
 #ifndef RG_LIGHT_TILES_PER_WAVE
 #define RG_LIGHT_TILES_PER_WAVE 16
-#endif
-#ifndef RG_LIGHT_CAP_MUL
-// light path, device-resident launches: a wave may take this many times its share of tiles
-// (the grid is still sized by the share), so waves whose tiles are cheap take more of them and
-// the queue drains evenly instead of every wave rendering exactly its share
-#define RG_LIGHT_CAP_MUL 1
 #endif
 #ifndef RG_HEAVY_TILES_PER_WAVE
 #define RG_HEAVY_TILES_PER_WAVE 0  // heavy path: 0 = persistent blocks (one per CU)
@@ -1815,37 +1252,8 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
-#ifndef RG_GLOBAL_FRAMES
-#define RG_GLOBAL_FRAMES 0  // every path: shading frames field-major in global memory (no scratch array)
-#endif
-#ifndef RG_LIGHT_GLOBAL_FRAMES
-#define RG_LIGHT_GLOBAL_FRAMES 0  // light path: shading frames field-major in global memory instead of a scratch array
-#endif
-#ifndef RG_TILE_PREFETCH
-// light path, device-resident launches: the next tile's queue slot is claimed at a tile's
-// start (round 4, same box, interleaved: test1 0.2972 -> 0.2939 ms over 200 frames, 0.3056 ->
-// 0.3043 over 20, test3 0.2656 -> 0.2631 over 20: profiles/r04/s21/session.txt, s22).  Not on
-// the heavy path: a claimed tile waits behind the wave's current (long) one, which lengthens
-// the frame's tail (north star 2.449 -> 2.463 ms)
-#define RG_TILE_PREFETCH 1
-#endif
-#ifndef RG_UNWIND_PRELOAD
-#define RG_UNWIND_PRELOAD 0  // unwind: a frame's kind and first four words read together
-#endif
-#ifndef RG_LIGHT_TEXEL_EARLY
-// light path: a textured hit's texel load is issued at the hit and converted after the lights'
-// setup, so its latency overlaps that work (test1 0.2979 -> 0.2955 ms over 200 frames, 20 frames
-// 0.3059 -> 0.3051, test3 equal; profiles/r04/s15/session.txt)
-#define RG_LIGHT_TEXEL_EARLY 1
-#endif
-#ifndef RG_PRIO_DEPTH
-#define RG_PRIO_DEPTH 0    // > 0: waves with a query at this recursion depth or deeper run at raised priority
-#endif
-#ifndef RG_LIGHT_TASKS
-#define RG_LIGHT_TASKS 0   // task splitting on the light path (kernel template parameter TASKS)
-#endif
 #ifndef RG_HEAVY_TASKS
-#define RG_HEAVY_TASKS 1   // ... and on the heavy path, for launches of fewer than RG_HEAVY_TASK_TILES tiles
+#define RG_HEAVY_TASKS 1   // task splitting on the heavy path, for launches of fewer than RG_HEAVY_TASK_TILES tiles
 #endif
 #ifndef RG_HEAVY_TASK_TILES
 // Task splitting shortens the slowest pixels' ray trees, which bound a small
@@ -1858,11 +1266,8 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 #ifndef RG_TASK_SLOTS
 #define RG_TASK_SLOTS 128
 #endif
-#ifndef RG_LIGHT_TASK_SLOTS
-#define RG_LIGHT_TASK_SLOTS 32  // light path: the pool of a one-wave block (a few KB of LDS, not ~10)
-#endif
-template <int S>
-struct TaskPoolT {
+struct TaskPool {
+    static constexpr int S = RG_TASK_SLOTS;
     static_assert(S % 32 == 0, "whole bitmap words");
     double ray[S][6];  // published ray (origin, direction)
     float col[S][4];   // the subtree's colour once done
@@ -1873,23 +1278,15 @@ struct TaskPoolT {
     uint32_t pend_m[S / 32];  // 1 = published, not taken
     int busy;                 // waves of the block that hold work
 };
-// one pool per block: the heavy path's (a CU's 12 waves) and the light path's
-// (a one-wave block); a kernel allocates only the one its instantiation uses
-__shared__ TaskPoolT<RG_TASK_SLOTS> rg_pool_h;
-__shared__ TaskPoolT<RG_LIGHT_TASK_SLOTS> rg_pool_l;
-template <bool L>
-__device__ __forceinline__ auto &pool_of() {
-    if constexpr (L) return rg_pool_l;
-    else return rg_pool_h;
-}
-template <bool L>
-constexpr int pool_slots() { return L ? RG_LIGHT_TASK_SLOTS : RG_TASK_SLOTS; }
+// one pool per block (heavy path: a CU's 12 waves); allocated only by the kernels that split tasks
+__shared__ TaskPool rg_pool;
+__device__ __forceinline__ TaskPool &pool_of() { return rg_pool; }
+constexpr int pool_slots() { return RG_TASK_SLOTS; }
 
 #define RG_WG __HIP_MEMORY_SCOPE_WORKGROUP
-template <bool L>
 __device__ __forceinline__ void pool_init() {
-    auto &P = pool_of<L>();
-    constexpr int S = pool_slots<L>();
+    auto &P = pool_of();
+    constexpr int S = pool_slots();
     if (threadIdx.x < S / 32) {
         P.free_m[threadIdx.x] = ~0u;
         P.pend_m[threadIdx.x] = 0u;
@@ -1898,10 +1295,9 @@ __device__ __forceinline__ void pool_init() {
     if (threadIdx.x == 0) P.busy = 0;
 }
 // Claim a free slot (-1: pool full).  Lanes start at different words/bits.
-template <bool L>
 __device__ __forceinline__ int pool_alloc(int lane) {
-    auto &P = pool_of<L>();
-    constexpr int S = pool_slots<L>();
+    auto &P = pool_of();
+    constexpr int S = pool_slots();
     const int rot = (lane >> 2) & 31;
     for (int i = 0; i < S / 32; ++i) {
         const int w = (lane + i) & (S / 32 - 1);
@@ -1917,22 +1313,19 @@ __device__ __forceinline__ int pool_alloc(int lane) {
     }
     return -1;
 }
-template <bool L>
 __device__ __forceinline__ void pool_publish(int slot) {  // ray/depth/pix written before
-    __hip_atomic_fetch_or(&pool_of<L>().pend_m[slot >> 5], 1u << (slot & 31), __ATOMIC_RELEASE, RG_WG);
+    __hip_atomic_fetch_or(&pool_of().pend_m[slot >> 5], 1u << (slot & 31), __ATOMIC_RELEASE, RG_WG);
 }
-template <bool L>
 __device__ __forceinline__ bool pool_any_pending() {
     uint32_t m = 0u;
 #pragma unroll
-    for (int w = 0; w < pool_slots<L>() / 32; ++w) m |= __hip_atomic_load(&pool_of<L>().pend_m[w], __ATOMIC_RELAXED, RG_WG);
+    for (int w = 0; w < pool_slots() / 32; ++w) m |= __hip_atomic_load(&pool_of().pend_m[w], __ATOMIC_RELAXED, RG_WG);
     return m != 0u;
 }
 // Take the k-th pending task of a snapshot (k = rank among the wave's idle lanes).
-template <bool L>
 __device__ __forceinline__ int pool_take(int k) {
-    auto &P = pool_of<L>();
-    for (int w = 0; w < pool_slots<L>() / 32; ++w) {
+    auto &P = pool_of();
+    for (int w = 0; w < pool_slots() / 32; ++w) {
         uint32_t m = __hip_atomic_load(&P.pend_m[w], __ATOMIC_RELAXED, RG_WG);
         const int n = __builtin_popcount(m);
         if (k >= n) {
@@ -1946,26 +1339,22 @@ __device__ __forceinline__ int pool_take(int k) {
     }
     return -1;
 }
-template <bool L>
 __device__ __forceinline__ bool pool_reclaim(int slot) {  // owner: un-publish if still pending
     const uint32_t bit = 1u << (slot & 31);
-    return (__hip_atomic_fetch_and(&pool_of<L>().pend_m[slot >> 5], ~bit, __ATOMIC_ACQ_REL, RG_WG) & bit) != 0u;
+    return (__hip_atomic_fetch_and(&pool_of().pend_m[slot >> 5], ~bit, __ATOMIC_ACQ_REL, RG_WG) & bit) != 0u;
 }
-template <bool L>
 __device__ __forceinline__ void pool_finish(int slot, C3 c) {  // taker: result, then done
-    auto &P = pool_of<L>();
+    auto &P = pool_of();
     P.col[slot][0] = c.r;
     P.col[slot][1] = c.g;
     P.col[slot][2] = c.b;
     __hip_atomic_store(&P.done[slot], 1, __ATOMIC_RELEASE, RG_WG);
 }
-template <bool L>
 __device__ __forceinline__ bool pool_done(int slot) {
-    return __hip_atomic_load(&pool_of<L>().done[slot], __ATOMIC_ACQUIRE, RG_WG) != 0;
+    return __hip_atomic_load(&pool_of().done[slot], __ATOMIC_ACQUIRE, RG_WG) != 0;
 }
-template <bool L>
 __device__ __forceinline__ void pool_release(int slot) {  // owner: slot free again
-    auto &P = pool_of<L>();
+    auto &P = pool_of();
     __hip_atomic_store(&P.done[slot], 0, __ATOMIC_RELAXED, RG_WG);
     __hip_atomic_fetch_or(&P.free_m[slot >> 5], 1u << (slot & 31), __ATOMIC_RELEASE, RG_WG);
 }
@@ -1982,12 +1371,6 @@ using namespace rgk;
 #endif
 #ifndef RG_NQ
 #define RG_NQ 8   // tile-queue heads (see the kernel's tile loop)
-#endif
-#ifndef RG_Q_HOME_BY_BLOCK
-#define RG_Q_HOME_BY_BLOCK 1
-#endif
-#ifndef RG_Q_INTERLEAVE
-#define RG_Q_INTERLEAVE 1
 #endif
 #define RG_QUEUE_BASE 16   // counters[16 + 16*q]: head q, one 128-B line each
 #define RG_QUEUE_STRIDE 16
@@ -2026,8 +1409,7 @@ void rg_render_kernel(RgKernelArgs a) {
     const unsigned long long t_wave0 = wall_clock64();
     uint32_t wt_tiles = 0;
 #endif
-    constexpr bool PLIGHT = LB > 1;  // the light path's (smaller) task pool
-    constexpr bool GFRAMES = MAXD == 0 || RG_GLOBAL_FRAMES || (LB > 1 && RG_LIGHT_GLOBAL_FRAMES);
+    constexpr bool GFRAMES = MAXD == 0;
     // the launch context's other counter set (the previous launch's, read back
     // already: same stream) starts the next launch at zero -- no memset per frame
     if (blockIdx.x == 0 && a.counters_next)
@@ -2077,9 +1459,6 @@ void rg_render_kernel(RgKernelArgs a) {
         src.dk = reinterpret_cast<const RgDsk *>(smem + a.lds_dsk);
         src.bx = reinterpret_cast<const RgBox *>(smem + a.lds_box);
         src.nd = reinterpret_cast<const RgBvhNode *>(smem + a.lds_nodes);
-#if RG_WAVE_NODE_SCALAR
-        src.nds = rg_cptr(a.nodes);
-#endif
     } else {
         src.s = rg_cptr(a.sph);
         src.cc = rg_cptr(a.sph_cc);
@@ -2109,7 +1488,7 @@ void rg_render_kernel(RgKernelArgs a) {
         T.texs = a.texs;
     }
     if (TASKS || LSPH || LCOLD) {
-        if constexpr (TASKS) pool_init<PLIGHT>();
+        if constexpr (TASKS) pool_init();
         __syncthreads();
     }
 
@@ -2183,18 +1562,12 @@ void rg_render_kernel(RgKernelArgs a) {
     FrameStack<GFRAMES ? 0 : MAXD> stk;  // GFRAMES: field-major frames in a global buffer, no scratch array
     stk.init(a);
 
-    // Sharded tile queue: RG_NQ heads, each owning a contiguous band of tiles
-    // (one 128-B line per head).  A single head saturates at ~88 dequeues/us
-    // (MI355X_MICROARCH.md "dequeue"), i.e. ~1.5 ms for a 4K frame of 8x8
-    // tiles; a wave starts on head (global wave id % RG_NQ) and moves to the
-    // next head when its band is exhausted (work stealing for the tail).
-    const uint32_t gwave = blockIdx.x * (blockDim.x / 64u) + (threadIdx.x >> 6);
-#if RG_Q_HOME_BY_BLOCK
-    uint32_t qi = blockIdx.x % RG_NQ, qtried = 0;  // a CU's waves share a head: adjacent tiles per CU
-    (void)gwave;
-#else
-    uint32_t qi = gwave % RG_NQ, qtried = 0;
-#endif
+    // Sharded tile queue: RG_NQ heads, head q serving tiles q, q + RG_NQ, ... (one
+    // 128-B line per head).  A single head saturates at ~88 dequeues/us
+    // (MI355X_MICROARCH.md "dequeue"), i.e. ~1.5 ms for a 4K frame of 8x8 tiles.
+    // The waves of a block start on head (block % RG_NQ) -- adjacent tiles per CU --
+    // and move to the next head when theirs is drained (work stealing for the tail).
+    uint32_t qi = blockIdx.x % RG_NQ, qtried = 0;
     // Lane state.  A lane holds one pixel of the wave's 8x8 tile, or (task
     // splitting, TASKS) one published subtree of another lane of the block;
     // the wave takes the next tile when none of its lanes has work.
@@ -2219,13 +1592,11 @@ void rg_render_kernel(RgKernelArgs a) {
     uint32_t pixel = 0;        // image pixel index (error reports) of the lane's pixel or task
     int task = -1;             // pool slot whose subtree this lane computes (-1: its own pixel)
     bool tiles_left = true;    // the tile queue has not been found empty
-#if RG_TILE_PREFETCH
-    [[maybe_unused]] uint32_t pf_k = 0u;       // lane 0: the prefetched slot of head qi
+    [[maybe_unused]] uint32_t pf_k = 0u;       // lane 0: the prefetched slot of head qi (tile-slot prefetch)
     [[maybe_unused]] bool pf_valid = false;    // (wave-uniform) a slot is claimed
-#endif
     uint32_t my_tile = 0xFFFFFFFFu;  // the wave's current tile (published when done: a.tile_flags)
     [[maybe_unused]] uint32_t tiles_taken = 0;
-    [[maybe_unused]] bool counted = false;  // this wave is counted in pool_of<PLIGHT>().busy
+    [[maybe_unused]] bool counted = false;  // this wave is counted in pool_of().busy
 #ifdef RG_TILE_TIMES
     uint32_t cur_tile = 0xFFFFFFFFu;  // diagnostic: per-tile time into rgb[tile] (us), wave iterations
     unsigned long long t_tile = 0, t_query = 0;  // into rgb[ntiles + tile], start, query time
@@ -2270,17 +1641,13 @@ void rg_render_kernel(RgKernelArgs a) {
                             // ONE batch covers every light (n_lights <= LB on this path): set it
                             // up now, with the per-light shading factors (parked in LDS), so that
                             // no hit-point state (h, n, incident) has to survive the shadow pass
-#if RG_LIGHT_TEXEL_EARLY
                             // a textured hit's texel load goes out now and is converted after the
-                            // lights' setup below (its latency overlaps that work)
+                            // lights' setup below (its latency overlaps that work: test1 0.2979 ->
+                            // 0.2955 ms over 200 frames, profiles/r04/s15/session.txt)
                             const bool textured = m.coloration != RG_COLORATION_COLOR;
                             uint32_t texel = 0u;
                             if (textured) texel = texel_fetch(T.texs, m, b, h);
                             else { park[64 * PK_COL] = m.color[0]; park[64 * (PK_COL + 1)] = m.color[1]; park[64 * (PK_COL + 2)] = m.color[2]; }
-#else
-                            const C3 col = surface_color(T.texs, m, b, h);
-                            park[64 * PK_COL] = col.r; park[64 * (PK_COL + 1)] = col.g; park[64 * (PK_COL + 2)] = col.b;
-#endif
                             park[64 * PK_REFL] = m.albedo_pi;                       // rendering.rs:164
                             // how the batch's colour is used: 0 diffuse, 1 reflecting at the depth
                             // limit (mix with the default colour), 2 reflecting with a frame
@@ -2309,12 +1676,10 @@ void rg_render_kernel(RgKernelArgs a) {
                                     sb.ld[l] = 0.0;
                                 }
                             }
-#if RG_LIGHT_TEXEL_EARLY
                             if (textured) {
                                 const C3 col = texel_color(texel);
                                 park[64 * PK_COL] = col.r; park[64 * (PK_COL + 1)] = col.g; park[64 * (PK_COL + 2)] = col.b;
                             }
-#endif
                             if (a.n_lights > 0) mode = MODE_SHADOW;
                             else shade = true;  // no lights: finish with black (rendering.rs:138)
                         } else {
@@ -2355,14 +1720,14 @@ void rg_render_kernel(RgKernelArgs a) {
                                     if (transmission(n, q.d, h, m.index, tr)) {
                                         trace_t = true;
                                         const Ray rr = reflection(n, q.d, h);
-                                        const int slot = pool_alloc<PLIGHT>(lane);
+                                        const int slot = pool_alloc(lane);
                                         if (slot >= 0) {
-                                            double *pr = pool_of<PLIGHT>().ray[slot];
+                                            double *pr = pool_of().ray[slot];
                                             pr[0] = rr.o.x; pr[1] = rr.o.y; pr[2] = rr.o.z;
                                             pr[3] = rr.d.x; pr[4] = rr.d.y; pr[5] = rr.d.z;
-                                            pool_of<PLIGHT>().depth[slot] = cd;
-                                            pool_of<PLIGHT>().pix[slot] = pixel;
-                                            pool_publish<PLIGHT>(slot);
+                                            pool_of().depth[slot] = cd;
+                                            pool_of().pix[slot] = pixel;
+                                            pool_publish(slot);
                                             f.type = FR_REFR_TASK | (slot << 8);
                                         } else {
                                             f.type = FR_REFR_T;
@@ -2511,7 +1876,7 @@ void rg_render_kernel(RgKernelArgs a) {
                         bool handed = false;
                         if constexpr (TASKS) {
                             if (task >= 0) {  // a published subtree: hand its colour back
-                                pool_finish<PLIGHT>(task, ret);
+                                pool_finish(task, ret);
                                 task = -1;
                                 handed = true;
                             }
@@ -2535,11 +1900,11 @@ void rg_render_kernel(RgKernelArgs a) {
                             const int slot = f.type >> 8;
                             if (ftype == FR_REFR_TASK) {  // ret = the transmission subtree's colour
                                 f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
-                                if (pool_reclaim<PLIGHT>(slot)) {  // nobody took the reflection ray: trace it here
-                                    const double *r = pool_of<PLIGHT>().ray[slot];
+                                if (pool_reclaim(slot)) {  // nobody took the reflection ray: trace it here
+                                    const double *r = pool_of().ray[slot];
                                     q.o = v3(r[0], r[1], r[2]);
                                     q.d = v3(r[3], r[4], r[5]);
-                                    pool_release<PLIGHT>(slot);
+                                    pool_release(slot);
                                     f.type = FR_REFR_R;
                                     qdepth = f.cdepth;
                                     mode = MODE_CLOSEST;
@@ -2548,12 +1913,12 @@ void rg_render_kernel(RgKernelArgs a) {
                                 }
                                 f.type = FR_REFR_WAIT | (slot << 8);
                             }
-                            if (!pool_done<PLIGHT>(slot)) {  // another lane is still tracing it
+                            if (!pool_done(slot)) {  // another lane is still tracing it
                                 mode = MODE_WAIT;
                                 break;
                             }
-                            const C3 rc = c3(pool_of<PLIGHT>().col[slot][0], pool_of<PLIGHT>().col[slot][1], pool_of<PLIGHT>().col[slot][2]);
-                            pool_release<PLIGHT>(slot);
+                            const C3 rc = c3(pool_of().col[slot][0], pool_of().col[slot][1], pool_of().col[slot][2]);
+                            pool_release(slot);
                             const float kr = f.f[0];  // as FR_REFR_R below (rendering.rs:115-117)
                             C3 col = cadd(cscl(rc, kr), cscl(c3(f.f[5], f.f[6], f.f[7]), 1.0f - kr));
                             ret = cmul(cscl(col, f.f[1]), c3(f.f[2], f.f[3], f.f[4]));
@@ -2561,21 +1926,10 @@ void rg_render_kernel(RgKernelArgs a) {
                             continue;
                         }
                     }
-#if RG_UNWIND_PRELOAD
-                    // one memory round trip for the common frame: its kind and the reflection
-                    // frame's four words are read together, before the branch on the kind
-                    const int ftype0 = f.type;
-                    const float g0 = f.f[0], g1 = f.f[1], g2 = f.f[2], g3 = f.f[3];
-                    if (ftype0 == FR_REFL) {
-                        ret = cadd(cscl(c3(g0, g1, g2), 1.0f - g3), cscl(ret, g3));
-                        sp--;
-                    } else if (ftype0 == FR_REFR_T) {
-#else
                     if (f.type == FR_REFL) {
                         ret = cadd(cscl(c3(f.f[0], f.f[1], f.f[2]), 1.0f - f.f[3]), cscl(ret, f.f[3]));
                         sp--;
                     } else if (f.type == FR_REFR_T) {
-#endif
                         f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
                         f.type = FR_REFR_R;
                         q.o = v3(f.rr[0], f.rr[1], f.rr[2]);
@@ -2631,7 +1985,11 @@ void rg_render_kernel(RgKernelArgs a) {
             // ring mode: the queue hands out groups of RING consecutive tiles (one contiguous
             // run of host memory per ring flush: 4 KB with 64x1 tiles)
             const uint32_t qlimit = (RING > 0 && use_ring) ? (ntiles + RING - 1) / RING : ntiles;
-#if RG_TILE_PREFETCH
+            // Tile-slot prefetch (light path, device-resident launches): the slot claimed at the
+            // previous tile's start, so the atomic's round trip overlaps that tile (round 4, same
+            // box, interleaved: test1 0.2972 -> 0.2939 ms over 200 frames, test3 0.2656 -> 0.2631:
+            // profiles/r04/s21/session.txt, s22).  Not on the heavy path: a claimed tile waits
+            // behind the wave's current (long) one, which lengthens the tail (north star +0.6 %)
             if constexpr (!HOSTF && LB > 1) {
                 if (pf_valid) {  // the slot claimed at the previous tile's start
                     const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)pf_k, 0, 64));
@@ -2641,14 +1999,13 @@ void rg_render_kernel(RgKernelArgs a) {
                     pf_valid = false;
                 }
             }
-#endif
             while (tile == 0xFFFFFFFFu && qtried < RG_NQ) {
                 uint32_t k = 0;
                 if (lane == 0) k = atomicAdd(reinterpret_cast<unsigned int *>(&a.counters[RG_QUEUE_BASE + RG_QUEUE_STRIDE * qi]), 1u);
                 k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
-#if RG_Q_INTERLEAVE
                 // head q serves tiles q, q+NQ, q+2NQ, ...: the tiles in flight stay a
-                // compact raster-order band of the frame, as with a single head
+                // compact raster-order band of the frame, as with a single head (the slot
+                // prefetch above uses the same slot -> tile rule)
                 const unsigned long long t = (unsigned long long)k * RG_NQ + qi;
                 if (t < qlimit) {
                     tile = (uint32_t)t;
@@ -2661,27 +2018,20 @@ void rg_render_kernel(RgKernelArgs a) {
                     }
                     break;
                 }
-#else
-                const uint32_t lo = (uint32_t)(((unsigned long long)ntiles * qi) / RG_NQ);
-                const uint32_t hi = (uint32_t)(((unsigned long long)ntiles * (qi + 1)) / RG_NQ);
-                static_assert(RG_HOST_RING == 0, "ring mode needs the interleaved queue");
-                if (lo + k < hi) { tile = lo + k; break; }
-#endif
                 qi = (qi + 1) % RG_NQ;
                 ++qtried;
             }
             if (tile == 0xFFFFFFFFu) {
                 tiles_left = false;
             } else {
-                constexpr uint32_t kmax = MAXD == 0 || TPW < 0 ? 0u : LB > 1 ? (TPW > 0 ? (uint32_t)TPW : RG_LIGHT_TILES_PER_WAVE) *
-                                                                          (HOSTF ? 1u : (uint32_t)RG_LIGHT_CAP_MUL)
-                                                                 : RG_HEAVY_TILES_PER_WAVE;
+                constexpr uint32_t kmax = MAXD == 0 || TPW < 0 ? 0u
+                                          : LB > 1 ? (TPW > 0 ? (uint32_t)TPW : RG_LIGHT_TILES_PER_WAVE)
+                                                   : RG_HEAVY_TILES_PER_WAVE;
                 if constexpr (kmax > 0) {
                     // non-persistent: a wave renders at most kmax tiles, so the grid
                     // drains through the hardware dispatcher wave (block) by wave
                     if (++tiles_taken >= kmax) tiles_left = false;
                 }
-#if RG_TILE_PREFETCH
                 if constexpr (!HOSTF && LB > 1) {
                     // claim the wave's NEXT queue slot now: the atomic's round trip overlaps this
                     // tile's work instead of stalling the wave between tiles (the wave renders
@@ -2692,7 +2042,6 @@ void rg_render_kernel(RgKernelArgs a) {
                         pf_valid = true;
                     }
                 }
-#endif
                 if (a.tile_perm) tile = a.tile_perm[tile];  // scheduling order only; every tile is rendered once
 #ifdef RG_WAVE_TIMES
                 ++wt_tiles;
@@ -2793,16 +2142,16 @@ void rg_render_kernel(RgKernelArgs a) {
             // idle lanes take subtrees other lanes of the block published
             const bool idle = mode == MODE_DONE;
             const unsigned long long want = __ballot(idle);
-            if (want != 0ull && pool_any_pending<PLIGHT>()) {
+            if (want != 0ull && pool_any_pending()) {
                 if (idle) {
-                    const int slot = pool_take<PLIGHT>((int)__builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
+                    const int slot = pool_take((int)__builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u)));
                     if (slot >= 0) {
-                        const double *r = pool_of<PLIGHT>().ray[slot];
+                        const double *r = pool_of().ray[slot];
                         q.o = v3(r[0], r[1], r[2]);
                         q.d = v3(r[3], r[4], r[5]);
-                        qdepth = pool_of<PLIGHT>().depth[slot];
-                        pixel = pool_of<PLIGHT>().pix[slot];
+                        qdepth = pool_of().depth[slot];
+                        pixel = pool_of().pix[slot];
                         task = slot;
                         mode = MODE_CLOSEST;
                         n_sec++;  // the published reflection ray is traced here
@@ -2814,7 +2163,7 @@ void rg_render_kernel(RgKernelArgs a) {
         const bool wave_live = __any(live);
         if constexpr (TASKS) {
             if (wave_live != counted) {  // the block's count of waves holding work (helpers' exit test)
-                if (lane == 0) atomicAdd(&pool_of<PLIGHT>().busy, wave_live ? 1 : -1);
+                if (lane == 0) atomicAdd(&pool_of().busy, wave_live ? 1 : -1);
                 counted = wave_live;
             }
         }
@@ -2822,7 +2171,7 @@ void rg_render_kernel(RgKernelArgs a) {
             if (tiles_left) continue;
             if constexpr (!TASKS) break;
             // tiles exhausted: serve the block's tasks until no wave holds work
-            if (!pool_any_pending<PLIGHT>() && __hip_atomic_load(&pool_of<PLIGHT>().busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+            if (!pool_any_pending() && __hip_atomic_load(&pool_of().busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
                 break;
             __builtin_amdgcn_s_sleep(4);
             continue;
@@ -2861,15 +2210,6 @@ void rg_render_kernel(RgKernelArgs a) {
                     atomicAdd(&a.counters[15], (unsigned long long)__builtin_popcountll(all & ~shl));
                 }
             }
-        }
-#endif
-#if RG_PRIO_DEPTH > 0
-        // a wave deep in a ray tree (the slowest tiles' long chains, which bound a single launch's
-        // makespan) takes issue priority on its SIMD over waves on shallow work
-        {
-            const int myd = mode == MODE_CLOSEST ? qdepth : hdepth;
-            if (__any(querying && myd >= RG_PRIO_DEPTH)) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(0);
         }
 #endif
 #ifdef RG_TILE_TIMES
@@ -2927,10 +2267,8 @@ void rg_render_kernel(RgKernelArgs a) {
                             if (k == l) { rq.d = sb.d[k]; ld = sb.ld[k]; }
                         closest_init(c);
                     }
-#ifndef RG_DBG_NO_SEC_TRACE
                     bool unused = false;
                     trace_query<F32F, BVH>(a, src, rq, false, 0.0, c, unused);
-#endif
                     if (exact) {
                         if (c.id >= 0 && !(c.t > ld)) occl |= 1u << l;
                         if (c.nan && c.nhit >= 2) raise_error(a, pixel, RG_ERR_NAN_DISTANCE);
@@ -2939,9 +2277,7 @@ void rg_render_kernel(RgKernelArgs a) {
             }
             if (mode == MODE_SHADOW && !exact) {
                 occl = ~occl_full & ((1u << LB) - 1u);  // absent slots count as done
-#ifndef RG_DBG_NO_SHADOW_TRACE
-                trace_shadow<LB, F32F || RG_LIGHT_SHADOW_FILTER>(a, src, q.o, sb, (1u << LB) - 1u, occl);
-#endif
+                trace_shadow<LB>(a, src, q.o, sb, (1u << LB) - 1u, occl);
             }
         }
 #ifdef RG_TILE_TIMES
@@ -3198,9 +2534,6 @@ extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scra
 #ifndef RG_LIGHT_PERSIST_BLOCKS_PER_CU
 #define RG_LIGHT_PERSIST_BLOCKS_PER_CU 8  // light persistent launches: one-wave blocks per CU (2 per SIMD)
 #endif
-#ifndef RG_DEEP_FORCE
-#define RG_DEEP_FORCE 0  // 1: host-frame / deep light launches run exactly RG_DEEP_BLOCKS_PER_CU blocks per CU
-#endif
 #ifndef RG_DEEP_BLOCKS_PER_CU
 #define RG_DEEP_BLOCKS_PER_CU 8  // deep-stack light launches: resident one-wave blocks per CU (bounds the frame buffer)
 #endif
@@ -3253,11 +2586,11 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     int cus = 0, per_cu = 0;
     const hipError_t oe = occupancy(reinterpret_cast<const void *>(kern), threads, lds, cus, per_cu);
     if (oe != hipSuccess) return oe;
-    if (MAXD == 0 && LB > 1 && (RG_DEEP_FORCE || per_cu > RG_DEEP_BLOCKS_PER_CU)) per_cu = RG_DEEP_BLOCKS_PER_CU;
-    // light single launches, persistent waves (TPW < 0): the occupancy query answers 8 one-wave
-    // blocks per CU, while 4 waves per SIMD (128 VGPRs) are resident (RG_WAVE_TIMES: 4,050 waves
-    // of one test1 launch ran at once) -- the resident count is set explicitly
-    if (MAXD != 0 && LB > 1 && TPW < 0) per_cu = RG_LIGHT_PERSIST_BLOCKS_PER_CU;
+    if (MAXD == 0 && LB > 1 && per_cu > RG_DEEP_BLOCKS_PER_CU) per_cu = RG_DEEP_BLOCKS_PER_CU;
+    // light single launches, persistent waves (TPW < 0): RG_LIGHT_PERSIST_BLOCKS_PER_CU one-wave
+    // blocks per CU (2 per SIMD), never more than the occupancy query admits (a scene whose LDS
+    // copy allows fewer would otherwise start the extra blocks only after the queue drained)
+    if (MAXD != 0 && LB > 1 && TPW < 0) per_cu = std::min(per_cu, RG_LIGHT_PERSIST_BLOCKS_PER_CU);
     const unsigned long long tiles = rg_tile_count(*a);
     const unsigned long long waves = (unsigned long long)threads / 64u;
     unsigned long long blocks = (unsigned long long)cus * per_cu;
@@ -3284,8 +2617,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
         *grid_threads = (size_t)blocks * threads;
         return hipSuccess;
     }
-    constexpr bool GFRAMES = MAXD == 0 || RG_GLOBAL_FRAMES || (LB > 1 && RG_LIGHT_GLOBAL_FRAMES);
-    if (GFRAMES && (a->deep_stack == nullptr || (unsigned long long)a->deep_stride < blocks * threads))
+    if (MAXD == 0 && (a->deep_stack == nullptr || (unsigned long long)a->deep_stride < blocks * threads))
         return hipErrorInvalidValue;  // the caller sized the frame buffer for another grid
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), lds, stream, *a);
     return hipGetLastError();
@@ -3304,7 +2636,7 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
     // the BVH kernels also hold the static per-wave traversal stacks
     constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u) -
                                 (uint32_t)(MAXD != 0 ? 0 : (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) * 64 * 4) -  // tile_px
-                                (TASKS ? (uint32_t)(LB > 1 ? sizeof(TaskPoolT<RG_LIGHT_TASK_SLOTS>) : sizeof(TaskPoolT<RG_TASK_SLOTS>)) : 0u);
+                                (TASKS ? (uint32_t)sizeof(TaskPool) : 0u);
     if (a->lds_total_bytes <= budget)  // whole scene (empty sphere part if n_sph == 0)
         return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_total_bytes, stream, gt);
     if (a->n_sph > 0 && a->lds_hot_bytes <= budget)
@@ -3312,16 +2644,6 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
     return launch_one<MAXD, false, false, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_lstack_bytes, stream, gt);
 }
 
-#ifndef RG_LIGHT_BIG_TPW
-// Light path, launches of at least RG_LIGHT_BIG_TILES tiles (4K frames and their halves): more
-// tiles per wave (fewer wave starts and scene stagings per frame: round 3, 32 tiles, test1
-// 0.2980 -> 0.2956 ms over 200 frames, profiles/r03/late/ab_light_big_tpw.txt).  Round 4: a
-// launch is its slowest wave's tile chain, so 32-tile chains leave a long drain
-// at the end of a short sequence: with 16 tiles per wave the bench's 20-frame configuration runs
-// test1 0.3139 -> 0.3068 ms and test3 0.274 -> 0.2635 (200 frames: +0.6 % / equal;
-// profiles/r04/s13/session.txt).  0 = RG_LIGHT_TILES_PER_WAVE for every launch.
-#define RG_LIGHT_BIG_TPW 0
-#endif
 #ifndef RG_LIGHT_BIG_TILES
 #define RG_LIGHT_BIG_TILES 50000ull  // whole 4K frames and 1/2 shares (test1 1/2 share 0.1504 -> 0.1490 ms)
 #endif
@@ -3331,15 +2653,6 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 // share 0.183 -> 0.166 ms, its 8-device rehearsal 0.3175 -> 0.297 ms (2.8x -> 3.0x); test3
 // equal; 3 waves per SIMD: no gain (profiles/r04/s27/session.txt)
 #define RG_LIGHT_SINGLE_PERSISTENT 2
-#endif
-#ifndef RG_LIGHT_LATENCY_TASKS
-#define RG_LIGHT_LATENCY_TASKS 0  // light path: task splitting for single small launches (below RG_LIGHT_TASK_TILES)
-#endif
-#ifndef RG_LIGHT_TASK_TILES
-#define RG_LIGHT_TASK_TILES 50000ull
-#endif
-#ifndef RG_LIGHT_F32_FILTER
-#define RG_LIGHT_F32_FILTER false  // light path: f32 pre-filter in front of the exact sphere tests of closest-hit rays
 #endif
 #ifndef RG_LIGHT_WPS
 #define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
@@ -3360,20 +2673,9 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
             // wave render exactly that many tiles and the slowest wave's sum the makespan
             // (2: launches below RG_LIGHT_BIG_TILES tiles only -- rg_render_multi's shares and bands)
             if (!a->pipelined && (RG_LIGHT_SINGLE_PERSISTENT != 2 || rg_tile_count(*a) < RG_LIGHT_BIG_TILES))
-                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, RG_LIGHT_F32_FILTER, false, RG_LIGHT_TASKS, -1>(a, stream, gt);
+                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, -1>(a, stream, gt);
         }
-        if constexpr (MAXD != 0 && RG_LIGHT_LATENCY_TASKS && !RG_LIGHT_TASKS) {
-            // one small launch on its own (a single-shot share, rg_render_multi): its makespan is
-            // its slowest tiles' ray trees, so idle lanes of a wave take published subtrees
-            if (!a->pipelined && rg_tile_count(*a) < RG_LIGHT_TASK_TILES)
-                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, RG_LIGHT_F32_FILTER, false, true>(a, stream, gt);
-        }
-        if constexpr (MAXD != 0 && RG_LIGHT_BIG_TPW > 0) {
-            if (rg_tile_count(*a) >= RG_LIGHT_BIG_TILES)
-                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, RG_LIGHT_F32_FILTER, false, RG_LIGHT_TASKS,
-                                    RG_LIGHT_BIG_TPW>(a, stream, gt);
-        }
-        return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, RG_LIGHT_F32_FILTER, false, RG_LIGHT_TASKS>(a, stream, gt);
+        return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false>(a, stream, gt);
     }
 #endif
 #ifdef RG_DEV_LIGHT_ONLY  // development builds: resource reports of the light kernels only
@@ -3397,22 +2699,16 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
 extern "C" int rg_max_array_frames(void) { return 64; }
 
 // Does this launch keep its frames in the launch context's global buffer (the
-// host sizes it with rg_render_grid_threads)?  Depths above the arrays always;
-// light launches too when built with RG_LIGHT_GLOBAL_FRAMES (no scratch array).
+// host sizes it with rg_render_grid_threads)?  Depths above the arrays.
 extern "C" int rg_launch_global_frames(const RgKernelArgs *a, int maxd) {
-    return maxd > rg_max_array_frames() || RG_GLOBAL_FRAMES || (RG_LIGHT_GLOBAL_FRAMES && !rg_heavy_path(*a));
+    (void)a;
+    return maxd > rg_max_array_frames();
 }
 
-#ifndef RG_MAXD_SMALL
-#define RG_MAXD_SMALL 0  // > 0: also a frame array of this many frames (depth <= RG_MAXD_SMALL + 1 scenes)
-#endif
 static hipError_t dispatch_depth(const RgKernelArgs *a, int maxd, hipStream_t stream, size_t *gt) {
 #ifdef RG_DEV_ONE_DEPTH  // development builds: the MAXD = 8 instantiations only
     return maxd <= 8 ? launch_depth<8>(a, stream, gt) : hipErrorNotSupported;
 #else
-#if RG_MAXD_SMALL > 0
-    if (maxd <= RG_MAXD_SMALL) return launch_depth<RG_MAXD_SMALL>(a, stream, gt);
-#endif
     if (maxd <= 8) return launch_depth<8>(a, stream, gt);
     if (maxd <= 16) return launch_depth<16>(a, stream, gt);
     if (maxd <= 64) return launch_depth<64>(a, stream, gt);
@@ -3433,7 +2729,7 @@ extern "C" hipError_t rg_launch_trace(const RgKernelArgs *a, const double *rays,
                                       int32_t *body, hipStream_t stream) {
     dim3 grid((n + 255) / 256);
     // per-lane walk stacks (stride = block size): lane_stack entries + the spare slot
-    const size_t lds = a->lane_stack > 0 ? ((size_t)(a->lane_stack + 1) * 4u + RG_LANE_HELP_BYTES) * 256u : 0u;
+    const size_t lds = a->lane_stack > 0 ? ((size_t)(a->lane_stack + 1) * 4u) * 256u : 0u;
     hipLaunchKernelGGL(rg_trace_kernel, grid, dim3(256), lds, stream, *a, rays, n, dist, body);
     return hipGetLastError();
 }
