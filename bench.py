@@ -209,6 +209,40 @@ def roofline(key: str, frame_s: float, n_gpus: int, alg_bytes: int, tex: int, al
     return res, hbm
 
 
+def verify_enabled(args, world: int) -> bool:
+    """Rank 0 checks the gathered frame against a 1-rank render whenever frames are gathered
+    (N > 1, or the world-1 RCCL rehearsal): the first real multi-GPU run proves its frame before
+    it reports a rate.  At N = 1 without a gather it runs on request (--verify)."""
+    return bool(getattr(args, "verify", False)) or world > 1 or bool(getattr(args, "rccl_rehearsal", False))
+
+
+def check_frame(got, ref, world: int) -> bool:
+    """Byte-for-byte comparison of rank 0's assembled frame with the 1-rank render; a mismatch
+    ends the run with a non-zero status (no Mrays/s line is printed)."""
+    import numpy as np
+
+    got = np.asarray(got)
+    ok = got.shape == ref.shape and bool((got == ref).all())
+    if not ok:
+        bad = int((got != ref).any(axis=-1).sum()) if got.shape == ref.shape else -1
+        raise SystemExit(f"verification: the {world}-rank frame differs from the 1-rank render "
+                         f"({bad} pixels differ; shapes {got.shape} vs {ref.shape})")
+    return True
+
+
+def gather_rank_times(elapsed_s: float, steps: int, kernel_ms: float, world: int, rank: int):
+    """Every rank's own timed-loop wall time per frame and its single-launch share time, gathered
+    to every rank (object collective: gloo or RCCL), so a skewed rank is visible in the line."""
+    mine = {"rank": rank, "ms_per_step": round(elapsed_s / max(1, steps) * 1e3, 4), "share_kernel_ms": round(kernel_ms, 4)}
+    if world == 1:
+        return [mine]
+    import torch.distributed as dist
+
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    return sorted(out, key=lambda r: r["rank"])
+
+
 def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cpu: bool, size=None,
             steps=None, warmup=None, budget_s=None):
     """Time `steps` frames of `workload` on this rank (after `warmup`), frame
@@ -385,12 +419,13 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     torch.cuda.synchronize(dev)
     kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / len(events)
 
+    per_rank = gather_rank_times(elapsed, steps, kernel_ms, world, rank)
     tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt[0])
     verified = None
-    if getattr(args, "verify", False):
+    if verify_enabled(args, world):  # one extra frame, outside the timed region
         if native:
             step()
             finish()
@@ -407,9 +442,7 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
             import numpy as np
 
             got = final if isinstance(final, np.ndarray) else final.cpu().numpy()
-            verified = bool((got == ref).all())
-            if not verified:
-                raise SystemExit(f"--verify: the {world}-rank frame differs from the 1-rank render")
+            verified = check_frame(got, ref, world)
     if native:
         pipe.close()
     elif pipe is not None and pipe.streams:
@@ -468,6 +501,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
                       "box_margin": round(bvh.margin, 6), "near_origin_bound": round(bvh.origin_bound, 3)}
     if verified is not None:
         res["verified_against_1_rank_frame"] = verified
+    if world > 1 or args.rccl_rehearsal:
+        res["per_rank"] = per_rank  # each rank's own timed-loop ms per frame and single-launch share time
     if cpu:
         res["cpu_baseline"] = cpu_baseline(scene, W, H)
         res["gpu_over_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
@@ -616,7 +651,8 @@ def main() -> None:
     ap.add_argument("--share", type=int, default=1,
                     help="diagnostic at N=1: time rank 0's share of an S-way split (no gather); value counts its rays")
     ap.add_argument("--verify", action="store_true",
-                    help="rank 0 checks the gathered frame against a 1-rank render, byte for byte")
+                    help="rank 0 checks the frame against a 1-rank render, byte for byte (always at N > 1 and "
+                         "with --rccl-rehearsal; this flag adds it at N = 1)")
     ap.add_argument("--plan", action="store_true",
                     help="print this rank's launch plan (rank, world, device) as JSON and exit before any GPU work")
     args = ap.parse_args()
@@ -639,7 +675,8 @@ def main() -> None:
     if args.same_device:
         local_rank = 0
     if args.plan:
-        line = {"rank": rank, "world": world, "local_rank": local_rank, "n_gpus": world}
+        line = {"rank": rank, "world": world, "local_rank": local_rank, "n_gpus": world,
+                "verify_against_1_rank_frame": verify_enabled(args, world)}
         if args.backend == "gloo" and world > 1:  # rehearse the rendezvous without a GPU
             import torch.distributed as dist
 

@@ -42,7 +42,9 @@ typedef enum rg_status {
     RG_ERR_DEVICE = -10,            /* HIP runtime error */
     RG_ERR_OUT_OF_MEMORY = -11,
     RG_ERR_CANCELLED = -12,         /* streaming receiver dropped         rendering.rs:53-54 */
-    RG_ERR_COLLECTIVE = -13         /* rg_render_multi: RCCL missing or a collective failed */
+    RG_ERR_COLLECTIVE = -13,        /* rg_render_multi: RCCL missing or a collective failed */
+    RG_ERR_PENDING = -14            /* rg_frames_read_image: a frame batch still waits for its gather
+                                       (call rg_frames_flush on every rank first) */
 } rg_status;
 
 /* ------------------------------------------------------------------------

@@ -72,8 +72,8 @@ const uint8_t *rg_frames_image(const rg_frames *frames);
 /* Rank 0: copy the latest assembled image to host memory (height*width*4
  * bytes).  Local: it issues no collective, so when a batch of frames is still
  * waiting for its gather (batch 2, an odd number of steps since the last
- * gather) it returns RG_ERR_INVALID_ARGUMENT -- call rg_frames_flush on EVERY
- * rank first.  Otherwise it blocks until this rank's enqueued work is done and
+ * gather) it returns RG_ERR_PENDING -- call rg_frames_flush on EVERY rank
+ * first (a null argument or a rank other than 0 is RG_ERR_INVALID_ARGUMENT).  Otherwise it blocks until this rank's enqueued work is done and
  * returns what rg_frames_flush returns (the image is copied either way). */
 rg_status rg_frames_read_image(const rg_frames *frames, uint8_t *host_out);
 

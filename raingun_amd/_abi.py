@@ -25,6 +25,7 @@ RG_ERR_DEVICE = -10
 RG_ERR_OUT_OF_MEMORY = -11
 RG_ERR_CANCELLED = -12
 RG_ERR_COLLECTIVE = -13
+RG_ERR_PENDING = -14
 
 BODY_SPHERE, BODY_PLANE, BODY_DISK, BODY_AABB = 0, 1, 2, 3
 COLORATION_COLOR, COLORATION_TEXTURE = 0, 1

@@ -601,6 +601,7 @@ const char *rg_status_string(int32_t st) {
     case RG_ERR_OUT_OF_MEMORY: return "out of device memory";
     case RG_ERR_CANCELLED: return "cancelled by the tile callback";
     case RG_ERR_COLLECTIVE: return "RCCL unavailable or failed (rg_render_multi)";
+    case RG_ERR_PENDING: return "a frame batch waits for its gather: rg_frames_flush on every rank first";
     default: return "unknown status";
     }
 }

@@ -364,7 +364,8 @@ rg_status rg_frames_read_image(const rg_frames *f, uint8_t *host_out) {
     if (!f || !f->scene || !host_out || f->rank != 0) return RG_ERR_INVALID_ARGUMENT;
     // a batch still waiting for its gather needs rg_frames_flush on EVERY rank first: the
     // catch-up gather is a collective, which rank 0 must not start alone
-    if (f->pend_n > 0 || f->last < 0) return RG_ERR_INVALID_ARGUMENT;
+    if (f->pend_n > 0) return RG_ERR_PENDING;
+    if (f->last < 0) return RG_ERR_INVALID_ARGUMENT;  // no frame rendered yet
     const rg_status st = frames_sync_local(const_cast<rg_frames *>(f));
     if (st == RG_ERR_DEVICE) return st;
     if (!ok(hipMemcpy(host_out, f->image[f->last], (size_t)f->h * f->w * 4, hipMemcpyDeviceToHost)))

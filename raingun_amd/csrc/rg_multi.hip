@@ -432,6 +432,17 @@ rg_status render_direct_one(const rg_scene *s, rg_multi_res *m, uint8_t *dst, rg
     return merge_snaps(m, 1, stats);
 }
 
+// Is the page-locked frame mapped into every device's address space (a buffer the
+// library registered is portable; one pinned elsewhere may be mapped on its own device only)?
+bool mapped_on_all(const rg_multi_res *m, uint8_t *dst, size_t bytes) {
+    for (int i = 0; i < m->n; ++i)
+        if (!ok(hipSetDevice(m->devs[i])) || rg_host_device_ptr(dst, bytes) == nullptr) {
+            (void)hipGetLastError();
+            return false;
+        }
+    return true;
+}
+
 // Direct path: every device renders its tiles in K bands and copies each band
 // straight to its image rows in page-locked host memory over its own link.
 rg_status render_direct(const rg_scene *s, rg_multi_res *m, uint8_t *rgba_out, rg_stats *stats) {
@@ -444,8 +455,10 @@ rg_status render_direct(const rg_scene *s, rg_multi_res *m, uint8_t *rgba_out, r
     // automatic (bands 0): trace-heavy scenes into a page-locked frame render in one launch per
     // device (north star, one device's timeline 0.97 -> 0.87 ms); light scenes keep the bands,
     // whose array kernels render a small share faster than the host-frame kernels (test1 0.27-0.31
-    // vs 0.49 ms: profiles/r04/latency_s1.json)
-    if (!pageable && (s->multi_bands < 0 || (s->multi_bands == 0 && rg_heavy_path(rg_make_args(s)))))
+    // vs 0.49 ms: profiles/r04/latency_s1.json).  Only when every device can store into the frame
+    // (ADVICE r4): otherwise the banded DMA copies, which work for any page-locked buffer.
+    if (!pageable && (s->multi_bands < 0 || (s->multi_bands == 0 && rg_heavy_path(rg_make_args(s)))) &&
+        mapped_on_all(m, dst, frame_bytes))
         return render_direct_one(s, m, dst, stats);
     if (pageable) {
         if (!m->h_frame) {

@@ -279,12 +279,18 @@ class RcclComm:
             raise RuntimeError("libraingun_hip.so predates rg_comm_init_rank: rebuild it")
         n = self._lib.rg_comm_id_bytes()
         uid = (C.c_uint8 * n)()
+        status = _abi.RG_OK
         if rank == 0:
-            _abi.check(self._lib.rg_comm_unique_id(uid), "rg_comm_unique_id")
-        obj = [bytes(uid)]
+            status = int(self._lib.rg_comm_unique_id(uid))
+        # (status, id) travel together, so a failure on rank 0 raises on EVERY rank instead of
+        # leaving the others blocked in the broadcast; the source is group rank 0's global rank
+        obj = [(status, bytes(uid))]
         if world > 1:
-            dist.broadcast_object_list(obj, src=0, group=group)
-        uid = (C.c_uint8 * n).from_buffer_copy(obj[0])
+            src = 0 if group is None else dist.get_global_rank(group, 0)
+            dist.broadcast_object_list(obj, src=src, group=group)
+        status, raw = obj[0]
+        _abi.check(status, "rg_comm_unique_id (rank 0)")
+        uid = (C.c_uint8 * n).from_buffer_copy(raw)
         h = C.c_void_p()
         _abi.check(self._lib.rg_comm_init_rank(uid, world, rank, int(device), C.byref(h)), "rg_comm_init_rank")
         self.handle = h
@@ -332,8 +338,10 @@ class NativeFramePipeline:
         self._scene = scene
         scene_handle = getattr(scene, "handle", scene)
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        # the rank's device first: the id broadcast (NCCL object tensors) and rg_frames_create
+        # (it binds the current device) both use it
+        torch.cuda.set_device(dev)
         self.comm = RcclComm(rank, world, dev.index if dev.index is not None else torch.cuda.current_device(), group)
-        torch.cuda.set_device(dev)  # rg_frames_create binds the current device
         h = C.c_void_p()
         st = self._lib.rg_frames_create(scene_handle, width, height, tile_rows, rank, world, depth,
                                         self.comm.handle, C.c_void_p(self.comm.gather_fn), C.byref(h))

@@ -140,3 +140,62 @@ def test_frame_pipeline_single_rank_needs_no_collective():
     assert sorted(got) == list(range(K))
     for k in range(K):
         assert bool((got[k] == k).all())
+
+
+class _FakeCommLib:
+    """Stands in for libraingun_hip.so's rg_comm_* entry points (no GPU, no RCCL)."""
+
+    def __init__(self, fail_unique_id):
+        self.fail = fail_unique_id
+        self.init_calls = 0
+
+    def rg_comm_init_rank(self, *a):
+        self.init_calls += 1
+        return 0
+
+    def rg_comm_id_bytes(self):
+        return 128
+
+    def rg_comm_unique_id(self, uid):
+        if self.fail:
+            return -13  # RG_ERR_COLLECTIVE
+        for i in range(len(uid)):
+            uid[i] = (7 * i) & 0xFF
+        return 0
+
+    def rg_comm_gather_fn(self):
+        return 1
+
+    def rg_comm_destroy(self, h):
+        return 0
+
+
+def _comm_worker(rank, world, port, fail, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from raingun_amd import _abi
+        fake = _FakeCommLib(fail)
+        _abi.lib = lambda: fake  # this spawned process only
+        try:
+            c = rd.RcclComm(rank, world, 0)
+            res = "ok" if fake.init_calls == 1 and c.gather_fn == 1 else "bad"
+        except _abi.RaingunError as e:
+            res = f"raised {e.status}" if hasattr(e, "status") else "raised"
+        with open(os.path.join(out_dir, f"r{rank}"), "w") as f:
+            f.write(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", [False, True])
+def test_rccl_comm_id_failure_raises_on_every_rank(fail, tmp_path):
+    """rank 0's rg_comm_unique_id failing must not leave the other ranks blocked in the
+    id broadcast -- the status travels with the id and every rank raises (gloo, world 3)."""
+    world = 3
+    mp.spawn(_comm_worker, args=(world, _free_port(), fail, str(tmp_path)), nprocs=world, join=True)
+    res = [open(tmp_path / f"r{r}").read() for r in range(world)]
+    if fail:
+        assert all(r.startswith("raised") for r in res), res
+    else:
+        assert res == ["ok"] * world, res
