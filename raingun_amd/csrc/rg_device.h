@@ -188,9 +188,6 @@ struct RgKernelArgs {
     // nullable: the whole LDS arena [0, lds_total_bytes) as one device image (light path): a
     // block stages its scene copy with ONE unrolled loop instead of a loop per table
     const void *lds_blob;
-    // light path, device-resident frames (rg_kernels.hip LightFrames; set by the launcher): byte
-    // offset of the colour slots in dynamic LDS and the number of levels kept there
-    uint32_t lfr_off, lfr_nl;
 };
 
 __host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }

@@ -1176,75 +1176,6 @@ struct FrameStack<0> {
     }
 };
 
-// Light path, device-resident frames (depth <= 17): the open frames split by size and use, so the
-// kernel keeps no per-lane array (its scratch is its register spills only; a 704-B frame array
-// cost every dispatch ~37 us of scratch set-up and test1 140 MB/frame of writes).
-//  * colour slot, 16 B per level (a lane's stack index IS its recursion depth on this path):
-//      FR_REFL {D.rgb, r}  (rendering.rs:86-91);  FR_REFR_* {kr, tau, surf.r, surf.g}  (:100-117).
-//    Levels k < nl live in LDS behind the scene arena, slot-major ([k][thread] float4: one
-//    conflict-free ds_read/write_b128 per access); nl is what the block's LDS budget admits
-//    (launch_one).  Deeper levels use the first 16 B of their global record.
-//  * refraction extras in the global record (written by refractive hits only): 16 B {surf.b,
-//    Tc.rgb} (Tc = the transmission subtree's colour, once known), then the pending reflection
-//    ray (ray.rs:56-60), 48 B.  The 80-B record of level k of grid thread g is at
-//    deep_stack + (k * deep_stride + g) * 80: whole 16-B loads and stores.
-//  * the frame kinds, 2 bits per level, one LDS word per thread.
-struct LightFrames {
-    // addresses are recomputed from the kernel arguments (SGPRs) and the thread index at each
-    // access and the kinds word lives in LDS too, so the frames hold no VGPR across the kernel's
-    // loop (the light kernel runs at the 128-VGPR limit of 4 waves per SIMD)
-    const RgKernelArgs &a;
-    unsigned char *smem;
-    static constexpr int MAX_LEVELS = 16;
-    static constexpr uint32_t REC = 80;  // bytes per level and thread in the global buffer
-    __device__ __forceinline__ LightFrames(const RgKernelArgs &args, unsigned char *sm) : a(args), smem(sm) {}
-    // the thread index through an opaque move at every access: the compiler cannot hoist the
-    // frame addresses out of the kernel's loop and hold them in VGPRs for its whole life
-    __device__ __forceinline__ static uint32_t tid() {
-        uint32_t t;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((uint32_t)threadIdx.x));
-        return t;
-    }
-    __device__ __forceinline__ float4 *lds(int k) const {
-        return reinterpret_cast<float4 *>(smem + a.lfr_off) + ((uint32_t)k * blockDim.x + tid());
-    }
-    __device__ __forceinline__ float4 *rec(int k) const {  // the level's record, 5 x 16 B
-        return reinterpret_cast<float4 *>(static_cast<unsigned char *>(a.deep_stack) +
-                                          (size_t)((uint32_t)k * a.deep_stride + blockIdx.x * blockDim.x + tid()) * REC);
-    }
-    // FR_* of level k in bits 2k .. 2k+1 of this thread's kinds word (behind the nl slot levels);
-    // a level's kind is always written when its frame is pushed, so the word needs no reset
-    __device__ __forceinline__ uint32_t *kinds() const {
-        return reinterpret_cast<uint32_t *>(smem + a.lfr_off + a.lfr_nl * 16u * blockDim.x) + tid();
-    }
-    __device__ __forceinline__ int kind(int k) const { return (int)((*kinds() >> (2 * k)) & 3u); }
-    __device__ __forceinline__ void set_kind(int k, int t) {
-        uint32_t *w = kinds();
-        *w = (*w & ~(3u << (2 * k))) | ((uint32_t)t << (2 * k));
-    }
-    __device__ __forceinline__ float4 slot(int k) const { return k < (int)a.lfr_nl ? *lds(k) : rec(k)[0]; }
-    __device__ __forceinline__ void set_slot(int k, float4 v) {
-        if (k < (int)a.lfr_nl) *lds(k) = v;
-        else rec(k)[0] = v;
-    }
-    __device__ __forceinline__ float4 extra(int k) const { return rec(k)[1]; }  // {surf.b, Tc.rgb}
-    __device__ __forceinline__ void set_extra(int k, float4 v) { rec(k)[1] = v; }
-    __device__ __forceinline__ void set_ray(int k, const Ray &r) {
-        double2 *d = reinterpret_cast<double2 *>(rec(k) + 2);
-        d[0] = make_double2(r.o.x, r.o.y);
-        d[1] = make_double2(r.o.z, r.d.x);
-        d[2] = make_double2(r.d.y, r.d.z);
-    }
-    __device__ __forceinline__ Ray ray(int k) const {
-        const double2 *d = reinterpret_cast<const double2 *>(rec(k) + 2);
-        const double2 d0 = d[0], d1 = d[1], d2 = d[2];
-        Ray r;
-        r.o = v3(d0.x, d0.y, d1.x);
-        r.d = v3(d1.y, d2.x, d2.y);
-        return r;
-    }
-};
-
 
 __device__ __forceinline__ uint32_t out_row_to_y(const RgKernelArgs &a, uint32_t orow) {
     uint32_t tl = orow / a.tile_rows, r = orow - tl * a.tile_rows;
@@ -1479,7 +1410,6 @@ void rg_render_kernel(RgKernelArgs a) {
     uint32_t wt_tiles = 0;
 #endif
     constexpr bool GFRAMES = MAXD == 0;
-    constexpr bool LFR = LB > 1 && MAXD == 8;  // light path, device-resident frames: LightFrames (any depth <= 17)
     // the launch context's other counter set (the previous launch's, read back
     // already: same stream) starts the next launch at zero -- no memset per frame
     if (blockIdx.x == 0 && a.counters_next)
@@ -1629,9 +1559,8 @@ void rg_render_kernel(RgKernelArgs a) {
         nring = 0;
     };
     uint32_t n_prim = 0, n_shadow = 0, n_sec = 0;
-    FrameStack<GFRAMES ? 0 : (LFR ? 1 : MAXD)> stk;  // GFRAMES: field-major frames in a global buffer, no scratch array
+    FrameStack<GFRAMES ? 0 : MAXD> stk;  // GFRAMES: field-major frames in a global buffer, no scratch array
     stk.init(a);
-    [[maybe_unused]] LightFrames lf(a, smem);  // LFR: colour slots in LDS, refraction extras in a global buffer
 
     // Sharded tile queue: RG_NQ heads, head q serving tiles q, q + RG_NQ, ... (one
     // 128-B line per head).  A single head saturates at ~88 dequeues/us
@@ -1776,30 +1705,6 @@ void rg_render_kernel(RgKernelArgs a) {
                             C3 col = cadd(cscl(def, kr), cscl(def, 1.0f - kr));
                             ret = cmul(cscl(col, m.transparency), surf);
                             unwind = true;
-                        } else if constexpr (LFR) {
-                            // colour slot {kr, tau, surf.r, surf.g}; surf.b, the pending reflection
-                            // ray (ray.rs:56-60) and later Tc in the level's global record
-                            lf.set_slot(sp, make_float4(kr, m.transparency, surf.r, surf.g));
-                            bool trace_t = false;
-                            if (kr < 1.0f) {
-                                // rendering.rs:100-113: the transmission subtree is traced first; the
-                                // reflection ray is stored BEFORE the transmission ray is built (into
-                                // q, written only on success): fewer live values
-                                lf.set_ray(sp, reflection(n, q.d, h));
-                                lf.set_extra(sp, make_float4(surf.b, 0.0f, 0.0f, 0.0f));
-                                lf.set_kind(sp, FR_REFR_T);
-                                trace_t = transmission(n, q.d, h, m.index, q);
-                                if (!trace_t) raise_error(a, pixel, RG_ERR_TRANSMISSION);
-                            }
-                            if (!trace_t) {  // kr >= 1 (or the transmission panic): refraction colour = default
-                                lf.set_kind(sp, FR_REFR_R);
-                                lf.set_extra(sp, make_float4(surf.b, def.r, def.g, def.b));
-                                q = reflection(n, q.d, h);
-                            }
-                            sp++;
-                            qdepth = cd;
-                            mode = MODE_CLOSEST;
-                            n_sec++;
                         } else {
                             auto &&f = stk[sp++];
                             f.f[0] = kr; f.f[1] = m.transparency;
@@ -1883,15 +1788,9 @@ void rg_render_kernel(RgKernelArgs a) {
                         ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
                         unwind = true;
                     } else {
-                        if constexpr (LFR) {  // rendering.rs:88
-                            lf.set_slot(sp, make_float4(dcol.r, dcol.g, dcol.b, park[64 * PK_R]));
-                            lf.set_kind(sp, FR_REFL);
-                            sp++;
-                        } else {
-                            auto &&f = stk[sp++];  // rendering.rs:88
-                            f.type = FR_REFL;
-                            f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = park[64 * PK_R];
-                        }
+                        auto &&f = stk[sp++];  // rendering.rs:88
+                        f.type = FR_REFL;
+                        f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = park[64 * PK_R];
                         // q = the reflection ray (origin = the shadow origin, direction set at the hit)
                         // without task splitting the stack index is the depth; a lane tracing a pooled
                         // subtree starts at sp = 0 with a non-zero depth, so TASKS keeps the hit's depth
@@ -1993,32 +1892,6 @@ void rg_render_kernel(RgKernelArgs a) {
                         }
                         mode = MODE_DONE;
                         break;
-                    }
-                    if constexpr (LFR) {
-                        const int k = sp - 1;
-                        const int kind = lf.kind(k);
-                        if (kind == FR_REFR_T) {  // ret = the transmission subtree's colour: trace the reflection ray
-                            float4 x = lf.extra(k);  // keeps surf.b
-                            x.y = ret.r; x.z = ret.g; x.w = ret.b;
-                            lf.set_extra(k, x);
-                            lf.set_kind(k, FR_REFR_R);
-                            q = lf.ray(k);
-                            qdepth = sp;  // the stack index is the depth
-                            mode = MODE_CLOSEST;
-                            n_sec++;
-                            break;
-                        }
-                        const float4 fs = lf.slot(k);
-                        if (kind == FR_REFL) {  // rendering.rs:86-91
-                            ret = cadd(cscl(c3(fs.x, fs.y, fs.z), 1.0f - fs.w), cscl(ret, fs.w));
-                        } else {  // FR_REFR_R (rendering.rs:115-117)
-                            const float kr = fs.x;
-                            const float4 x = lf.extra(k);  // {surf.b, Tc.rgb}
-                            C3 col = cadd(cscl(ret, kr), cscl(c3(x.y, x.z, x.w), 1.0f - kr));
-                            ret = cmul(cscl(col, fs.y), c3(fs.z, fs.w, x.x));
-                        }
-                        sp--;
-                        continue;
                     }
                     auto &&f = stk[sp - 1];
                     if constexpr (TASKS) {
@@ -2658,9 +2531,6 @@ extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scra
 // ---------------------------------------------------------------- launchers
 // One persistent block per CU slot: grid = CUs x (blocks per CU the register
 // and LDS budgets admit), capped by the tiles the frame has.
-#ifndef RG_LIGHT_WPS
-#define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
-#endif
 #ifndef RG_LIGHT_PERSIST_BLOCKS_PER_CU
 #define RG_LIGHT_PERSIST_BLOCKS_PER_CU 8  // light persistent launches: one-wave blocks per CU (2 per SIMD)
 #endif
@@ -2700,30 +2570,8 @@ static hipError_t occupancy(const void *kern, int threads, size_t lds, int &cus,
     return hipSuccess;
 }
 
-// Static LDS of a kernel (its __shared__ arrays), cached per kernel.
-static std::mutex lds_mu;
-static std::vector<std::pair<const void *, uint32_t>> lds_cache;
-static hipError_t static_lds(const void *kern, uint32_t &bytes) {
-    std::lock_guard<std::mutex> g(lds_mu);
-    for (const auto &e : lds_cache)
-        if (e.first == kern) {
-            bytes = e.second;
-            return hipSuccess;
-        }
-    hipFuncAttributes attr;
-    if (hipFuncGetAttributes(&attr, kern) != hipSuccess) return hipErrorInvalidValue;
-    bytes = (uint32_t)attr.sharedSizeBytes;
-    lds_cache.push_back({kern, bytes});
-    return hipSuccess;
-}
-
-#ifndef RG_LIGHT_LDS_BLOCK
-// LDS per one-wave light block at which RG_LIGHT_WPS waves per SIMD stay resident (160 KiB over 16)
-#define RG_LIGHT_LDS_BLOCK (160u * 1024u / (4u * RG_LIGHT_WPS))
-#endif
-
 // Launch (or, with grid_threads != nullptr, only size: the threads of the
-// grid, which a MAXD == 0 or LightFrames launch needs for its frame buffer) one instantiation.
+// grid, which a MAXD == 0 launch needs for its frame buffer) one instantiation.
 template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0>
 static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream, size_t *grid_threads) {
     // Block size.  The heavy path shares one LDS copy of the scene (and the
@@ -2735,25 +2583,6 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     // slowest wave -- one refractive tile -- is done).
     constexpr int threads = LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS;  // LB > 1: the light path
     auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH, TASKS, TPW>;
-    constexpr bool LFR = LB > 1 && MAXD == 8;  // light path, device-resident frames (LightFrames)
-    RgKernelArgs la;
-    if constexpr (LFR) {
-        // the colour slots of the first nl frame levels go behind the scene arena in dynamic LDS:
-        // as many levels as fit the block's share of the CU's LDS at RG_LIGHT_WPS waves per SIMD
-        // (deeper levels use the global records)
-        la = *a;
-        uint32_t stat = 0;
-        if (static_lds(reinterpret_cast<const void *>(kern), stat) != hipSuccess) return hipErrorInvalidValue;
-        const uint32_t off = (uint32_t)((lds + 15) & ~(size_t)15), slot_bytes = 16u * (uint32_t)threads;
-        const uint32_t levels = a->max_depth > 1 ? a->max_depth - 1 : 0u;
-        const uint32_t kinds_bytes = 4u * (uint32_t)threads;  // LightFrames::kinds
-        const uint32_t used = stat + off + kinds_bytes;
-        const uint32_t room = RG_LIGHT_LDS_BLOCK > used ? RG_LIGHT_LDS_BLOCK - used : 0u;
-        la.lfr_off = off;
-        la.lfr_nl = std::min(levels, room / slot_bytes);
-        lds = (size_t)off + (size_t)la.lfr_nl * slot_bytes + kinds_bytes;
-        a = &la;
-    }
     int cus = 0, per_cu = 0;
     const hipError_t oe = occupancy(reinterpret_cast<const void *>(kern), threads, lds, cus, per_cu);
     if (oe != hipSuccess) return oe;
@@ -2782,16 +2611,13 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     constexpr unsigned long long kmax = MAXD == 0 || TPW < 0 ? 0 : LB > 1 ? (TPW > 0 ? TPW : RG_LIGHT_TILES_PER_WAVE) : RG_HEAVY_TILES_PER_WAVE;
     if constexpr (kmax > 0)  // non-persistent: one wave per kmax tiles
         blocks = (tiles + waves * kmax - 1) / (waves * kmax);
-    if (a->max_grid_threads && blocks * threads > a->max_grid_threads) {
-        if (kmax > 0) return hipErrorInvalidConfiguration;  // a wave per kmax tiles: the grid cannot shrink
-        blocks = a->max_grid_threads / threads;
-    }
+    if (a->max_grid_threads && blocks * threads > a->max_grid_threads) blocks = a->max_grid_threads / threads;
     if (blocks < 1) blocks = 1;
     if (grid_threads) {
         *grid_threads = (size_t)blocks * threads;
         return hipSuccess;
     }
-    if ((MAXD == 0 || LFR) && (a->deep_stack == nullptr || (unsigned long long)a->deep_stride < blocks * threads))
+    if (MAXD == 0 && (a->deep_stack == nullptr || (unsigned long long)a->deep_stride < blocks * threads))
         return hipErrorInvalidValue;  // the caller sized the frame buffer for another grid
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), lds, stream, *a);
     return hipGetLastError();
@@ -2828,6 +2654,9 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 // equal; 3 waves per SIMD: no gain (profiles/r04/s27/session.txt)
 #define RG_LIGHT_SINGLE_PERSISTENT 2
 #endif
+#ifndef RG_LIGHT_WPS
+#define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
+#endif
 
 template <int MAXD>
 static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t *gt) {
@@ -2838,21 +2667,15 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
     const bool heavy = rg_heavy_path(*a);
 #ifndef RG_DEV_HEAVY_ONLY  // development builds: resource reports of the heavy kernels only
     if (!heavy) {
-        // frame levels <= LightFrames::MAX_LEVELS run the MAXD = 8 (LightFrames) kernels whatever
-        // their depth (dispatch_depth); deeper ones the 64-frame arrays or the global frames
-        if constexpr (MAXD == 16) return hipErrorInvalidValue;
-        if constexpr (MAXD != 0 && MAXD != 16) {
+        if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT) {
             // a launch on its own (not one of several frames in flight): persistent waves at full
             // occupancy balance the tiles dynamically, where a fixed tiles-per-wave grid makes every
             // wave render exactly that many tiles and the slowest wave's sum the makespan
-            // (2: launches below RG_LIGHT_BIG_TILES tiles only -- rg_render_multi's shares and bands).
-            // A launch whose frame buffer had to be bounded (max_grid_threads) is persistent too.
-            if ((RG_LIGHT_SINGLE_PERSISTENT && !a->pipelined &&
-                 (RG_LIGHT_SINGLE_PERSISTENT != 2 || rg_tile_count(*a) < RG_LIGHT_BIG_TILES)) ||
-                a->max_grid_threads != 0)
+            // (2: launches below RG_LIGHT_BIG_TILES tiles only -- rg_render_multi's shares and bands)
+            if (!a->pipelined && (RG_LIGHT_SINGLE_PERSISTENT != 2 || rg_tile_count(*a) < RG_LIGHT_BIG_TILES))
                 return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, -1>(a, stream, gt);
         }
-        if constexpr (MAXD != 16) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false>(a, stream, gt);
+        return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false>(a, stream, gt);
     }
 #endif
 #ifdef RG_DEV_LIGHT_ONLY  // development builds: resource reports of the light kernels only
@@ -2876,19 +2699,17 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
 extern "C" int rg_max_array_frames(void) { return 64; }
 
 // Does this launch keep its frames in the launch context's global buffer (the
-// host sizes it with rg_render_grid_threads)?  Depths above the arrays, and light launches.
+// host sizes it with rg_render_grid_threads)?  Depths above the arrays.
 extern "C" int rg_launch_global_frames(const RgKernelArgs *a, int maxd) {
-    // light path: LightFrames keep the refraction extras (and levels beyond LDS) in the buffer too
-    return maxd > rg_max_array_frames() || (!rg_heavy_path(*a) && maxd <= LightFrames::MAX_LEVELS);
+    (void)a;
+    return maxd > rg_max_array_frames();
 }
 
 static hipError_t dispatch_depth(const RgKernelArgs *a, int maxd, hipStream_t stream, size_t *gt) {
-    // light path: LightFrames (MAXD = 8 kernels) for up to MAX_LEVELS frame levels
-    const bool lfr = !rg_heavy_path(*a) && maxd <= LightFrames::MAX_LEVELS;
 #ifdef RG_DEV_ONE_DEPTH  // development builds: the MAXD = 8 instantiations only
-    return maxd <= 8 || lfr ? launch_depth<8>(a, stream, gt) : hipErrorNotSupported;
+    return maxd <= 8 ? launch_depth<8>(a, stream, gt) : hipErrorNotSupported;
 #else
-    if (maxd <= 8 || lfr) return launch_depth<8>(a, stream, gt);
+    if (maxd <= 8) return launch_depth<8>(a, stream, gt);
     if (maxd <= 16) return launch_depth<16>(a, stream, gt);
     if (maxd <= 64) return launch_depth<64>(a, stream, gt);
     return launch_depth<0>(a, stream, gt);
