@@ -33,6 +33,15 @@ typedef struct rg_bvh_info {
 rg_status rg_debug_set_bvh(rg_scene *scene, int32_t enable);
 rg_status rg_debug_bvh_info(const rg_scene *scene, rg_bvh_info *info);
 
+/* Shadow-ray light buffers (heavy path, BVH scenes; rg_lightbuf.cpp): per light,
+ * a grid whose cells list every sphere a shadow ray starting there could hit,
+ * so a shadow ray tests its cell's spheres instead of walking the BVH.  enable
+ * 1 (default) / 0 (the BVH walk for every shadow ray); results are identical
+ * either way.  rg_debug_lightbuf_count: lights with a buffer (0 when none was
+ * built or the BVH is off). */
+rg_status rg_debug_set_lightbuf(rg_scene *scene, int32_t enable);
+int32_t rg_debug_lightbuf_count(const rg_scene *scene);
+
 /* BVH walk per ray kind: rays at recursion depth >= min_depth (secondary rays
  * and the shadow rays of their hits: incoherent) walk the tree per lane with a
  * nearest-first stack; shallower rays walk it wave-coherently.  0 = every

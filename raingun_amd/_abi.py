@@ -139,6 +139,7 @@ EXPORTED_SYMBOLS = (
 )
 # include/raingun_debug.h
 DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
+                 "rg_debug_set_lightbuf", "rg_debug_lightbuf_count",
                  "rg_debug_set_tile_order", "rg_debug_set_lane_depth", "rg_debug_set_image_bands",
                  "rg_debug_set_host_tile_shape", "rg_debug_set_multi", "rg_debug_gather_noop")
 # include/raingun_frames.h
@@ -193,6 +194,11 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_set_path.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_set_bvh.restype = C.c_int32
     lib.rg_debug_set_bvh.argtypes = [C.c_void_p, C.c_int32]
+    if hasattr(lib, "rg_debug_set_lightbuf"):  # absent from older builds A/B runs load (RAINGUN_HIP_LIB)
+        lib.rg_debug_set_lightbuf.restype = C.c_int32
+        lib.rg_debug_set_lightbuf.argtypes = [C.c_void_p, C.c_int32]
+        lib.rg_debug_lightbuf_count.restype = C.c_int32
+        lib.rg_debug_lightbuf_count.argtypes = [C.c_void_p]
     lib.rg_debug_bvh_info.restype = C.c_int32
     lib.rg_debug_bvh_info.argtypes = [C.c_void_p, P(rg_bvh_info)]
     lib.rg_debug_set_tile_order.restype = C.c_int32

@@ -24,6 +24,7 @@
 #include "../../include/raingun_debug.h"
 #include "rg_bvh.h"
 #include "rg_device.h"
+#include "rg_lightbuf.h"
 #include "rg_internal.h"
 
 #pragma clang fp contract(off)
@@ -221,6 +222,12 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
     a.bvh_rbound = s->bvh_rbound;
     a.bvh_margin = s->bvh_margin;
     a.bvh_extent = s->bvh_extent;
+    // light buffers only with the BVH (the margins use its bounds; the kernel takes them on the BVH path)
+    const bool lbuf = bvh && s->lbuf_enabled && s->n_lbuf > 0;
+    a.lbuf = lbuf ? s->lbuf : nullptr;
+    a.lb_start = lbuf ? s->lb_start : nullptr;
+    a.lb_ent = lbuf ? s->lb_ent : nullptr;
+    a.n_lbuf = lbuf ? s->n_lbuf : 0;
     a.bodies = s->bodies;
     a.mats = s->mats;
     a.lights = s->lights;
@@ -479,6 +486,9 @@ rg_status upload_tables(rg_scene *s, const rg_host_tables &h) {
     RG_UP(mats, mats);
     RG_UP(lights, lights);
     RG_UP(nodes, nodes);
+    RG_UP(lbuf, lbuf);
+    RG_UP(lb_start, lb_start);
+    RG_UP(lb_ent, lb_ent);
 #undef RG_UP
     // textures: RGBA8 -> one u32 per texel (one 4-byte gather per lookup)
     std::vector<RgTexDev> texs(h.tex_w.size());
@@ -546,6 +556,7 @@ void copy_scalars(rg_scene *dst, const rg_scene *src) {
     dst->n_lights = src->n_lights;
     dst->n_textures = src->n_textures;
     dst->n_nodes = src->n_nodes;
+    dst->n_lbuf = src->n_lbuf;
     dst->lane_stack = src->lane_stack;
     dst->nan_scene = src->nan_scene;
     dst->bvh_obound = src->bvh_obound;
@@ -580,6 +591,7 @@ void rg_sync_settings(rg_scene *dst, const rg_scene *src) {
     dst->max_depth = src->max_depth;
     dst->path = src->path;
     dst->bvh_enabled = src->bvh_enabled;
+    dst->lbuf_enabled = src->lbuf_enabled;
     dst->lane_min_depth = src->lane_min_depth;
     dst->tile_order = src->tile_order;
 }
@@ -752,6 +764,35 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         ld.dn[1] = ny * inv;
         ld.dn[2] = nz * inv;
         ld.pad2 = 0.0;
+    }
+    // Shadow-ray light buffers (rg_lightbuf.cpp) over the BVH-ordered sphere tables, for the first
+    // RG_LB_MAX_LIGHTS lights; a light that cannot be served well keeps the BVH walk (kind NONE)
+    if (!h.nodes.empty()) {
+        std::vector<double> sp(4 * h.sph.size());
+        for (size_t j = 0; j < h.sph.size(); ++j) {
+            const double *p = &sph_raw[4 * (size_t)bvh.order[j]];  // centre, radius of BVH position j
+            std::memcpy(&sp[4 * j], p, 4 * sizeof(double));
+        }
+        const uint32_t nl = std::min<uint32_t>(d->n_lights, RG_LB_MAX_LIGHTS);
+        h.lbuf.assign(nl, RgLightBufDev{});
+        int built = 0;
+        for (uint32_t i = 0; i < nl; ++i) {
+            RgLightBufBuild lb;
+            if (!rg_build_lightbuf(sp.data(), (int)h.sph.size(), h.lights[i].kind, h.lights[i].dn, h.lights[i].v,
+                                   bvh.extent, (double)bvh.obound, lb))
+                continue;
+            const uint32_t ebase = (uint32_t)h.lb_ent.size(), cbase = (uint32_t)h.lb_start.size();
+            for (uint32_t &v : lb.start) v += ebase;
+            lb.dev.cell_off = cbase;
+            lb.dev.always0 += ebase;
+            lb.dev.always1 += ebase;
+            h.lb_start.insert(h.lb_start.end(), lb.start.begin(), lb.start.end());
+            h.lb_ent.insert(h.lb_ent.end(), lb.ent.begin(), lb.ent.end());
+            h.lbuf[i] = lb.dev;
+            ++built;
+        }
+        if (!built) h.lbuf.clear();
+        s->n_lbuf = (int32_t)h.lbuf.size();
     }
     h.tex_w.resize(d->n_textures);
     h.tex_h.resize(d->n_textures);
@@ -1362,6 +1403,19 @@ rg_status rg_debug_set_bvh(rg_scene *s, int32_t enable) {
     if (!s || (enable != 0 && enable != 1)) return RG_ERR_INVALID_ARGUMENT;
     s->bvh_enabled = enable != 0;
     return RG_OK;
+}
+
+rg_status rg_debug_set_lightbuf(rg_scene *s, int32_t enable) {
+    if (!s || (enable != 0 && enable != 1)) return RG_ERR_INVALID_ARGUMENT;
+    s->lbuf_enabled = enable != 0;
+    return RG_OK;
+}
+
+int32_t rg_debug_lightbuf_count(const rg_scene *s) {
+    if (!s || !s->host || !s->bvh_enabled || s->n_nodes == 0) return 0;
+    int32_t n = 0;
+    for (const RgLightBufDev &b : s->host->lbuf) n += b.kind != RG_LB_NONE;
+    return n;
 }
 
 rg_status rg_debug_bvh_info(const rg_scene *s, rg_bvh_info *info) {

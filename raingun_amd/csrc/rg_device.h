@@ -90,6 +90,8 @@ struct RgLightDev {        // lights.rs:8-26
     double pad2;              // 80 B: 16-B multiple for LDS staging
 };
 
+struct RgLightBufDev;  // rg_lightbuf_ray.h
+
 struct RgTexDev {
     const uint32_t *texels;  // RGBA8 packed little-endian: r | g<<8 | b<<16 | a<<24
     int32_t w, h;
@@ -188,6 +190,12 @@ struct RgKernelArgs {
     // nullable: the whole LDS arena [0, lds_total_bytes) as one device image (light path): a
     // block stages its scene copy with ONE unrolled loop instead of a loop per table
     const void *lds_blob;
+    // nullable: shadow-ray light buffers of the first n_lbuf lights (rg_lightbuf_ray.h); a light's
+    // shadow rays test only the spheres of their cell's list (heavy path, BVH scenes)
+    const RgLightBufDev *lbuf;
+    const uint32_t *lb_start;  // cell list starts (per light: cells + 1 words, at RgLightBufDev::cell_off)
+    const uint32_t *lb_ent;    // sphere positions of every list
+    int32_t n_lbuf;
 };
 
 __host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }

@@ -12,6 +12,7 @@
 #include "../../include/raingun.h"
 #include "../../include/raingun_debug.h"
 #include "rg_device.h"
+#include "rg_lightbuf_ray.h"
 
 // Per-stream launch state (ray counters, tile-queue heads, error words, tile
 // ordering scratch, deep frame buffer, timing events).  Launches on distinct
@@ -128,6 +129,8 @@ struct rg_host_tables {
     std::vector<RgMatDev> mats;
     std::vector<RgLightDev> lights;
     std::vector<RgBvhNode> nodes;
+    std::vector<RgLightBufDev> lbuf;           // per light (kind RG_LB_NONE: no buffer), first RG_LB_MAX_LIGHTS lights
+    std::vector<uint32_t> lb_start, lb_ent;    // every light's cell starts / list entries, concatenated
     std::vector<uint32_t> tex_w, tex_h;
     std::vector<std::vector<uint32_t>> texels;
 };
@@ -161,6 +164,10 @@ struct rg_scene {
     int32_t lane_stack = 0;      // per-lane walk stack entries the tree needs (0: per-lane walk unavailable)
     int32_t lane_min_depth = 1;  // rays of this depth and deeper walk the BVH per lane
     bool bvh_enabled = true;
+    RgLightBufDev *lbuf = nullptr;  // shadow-ray light buffers (rg_lightbuf.cpp), n_lbuf lights
+    uint32_t *lb_start = nullptr, *lb_ent = nullptr;
+    int32_t n_lbuf = 0;
+    bool lbuf_enabled = true;       // rg_debug_set_lightbuf
     float bvh_obound = 0.0f;
     double bvh_rbound = 0.0, bvh_margin = 0.0, bvh_extent = 0.0;
     rg_bvh_info bvh_info{};

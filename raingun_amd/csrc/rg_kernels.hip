@@ -28,6 +28,7 @@
 #include "../../include/raingun.h"
 #include "rg_bvh_ray.h"
 #include "rg_device.h"
+#include "rg_lightbuf_ray.h"
 
 #pragma clang fp contract(off)
 
@@ -673,6 +674,38 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
     RG_STAT(12, RG_CLOCK() - t_in);
 }
 
+// Shadow ray of light `light` through the light's buffer (rg_lightbuf_ray.h, rg_lightbuf.cpp):
+// the spheres of the ray's cell and of the light's always list, each with leaf_query's f32
+// pre-filter and exact test, in place of the BVH walk.  The lists hold every sphere the exact
+// test could accept for this ray, so the any-hit answer is the walk's.  false: the buffer does
+// not cover this ray (origin beyond the near-ray bound, no direction), the caller walks the BVH.
+template <class Src>
+__device__ __forceinline__ bool lbuf_spheres(const RgKernelArgs &a, const Src &src, int light, V3 o, V3 d, double ld,
+                                             bool &occl, bool &need) {
+    const RgLightBufDev &B = a.lbuf[light];
+    if (B.kind == RG_LB_NONE) return false;
+    double lx = 0.0, ly = 0.0, lz = 0.0;
+    if (B.kind == RG_LB_SPHERICAL) {
+        lx = a.lights[light].v[0];
+        ly = a.lights[light].v[1];
+        lz = a.lights[light].v[2];
+    }
+    const int cell = rg_lb_cell(B, lx, ly, lz, o.x, o.y, o.z, a.bvh_obound);
+    if (cell == RG_LB_SKIP) return false;
+    const RayF rf = make_rayf(o, d);
+    Closest unused;
+    closest_init(unused);
+    for (uint32_t k = B.always0; k < B.always1 && need; ++k)
+        leaf_query(a, src, (int)a.lb_ent[k], 1, o, d, rf, true, ld, unused, occl, need);
+    if (cell >= 0) {
+        const uint32_t *st = a.lb_start + B.cell_off + (uint32_t)cell;
+        const uint32_t k0 = st[0], k1 = st[1];
+        for (uint32_t k = k0; k < k1 && need; ++k)
+            leaf_query(a, src, (int)a.lb_ent[k], 1, o, d, rf, true, ld, unused, occl, need);
+    }
+    return true;
+}
+
 template <bool F32F, bool BVH, class Src>
 __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
     if constexpr (!BVH) sph_primary<F32F>(a, src, d, c);
@@ -721,7 +754,7 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
 // loops as soon as every lane that is still testing is a finished shadow ray.
 template <bool F32F, bool BVH, class Src>
 __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &src, const Ray &r, bool shadow, double ld,
-                                            Closest &c, bool &occl, bool lane_walk = false) {
+                                            Closest &c, bool &occl, bool lane_walk = false, int light = -1) {
     const V3 o = r.o, d = r.d;
     bool need = true;
     if constexpr (!BVH) {
@@ -776,7 +809,11 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
         const int cls = (need && !c.nan) ? rg_bvh_classify(a.bvh_obound, a.bvh_rbound, a.bvh_margin, a.bvh_extent,
                                                            o.x, o.y, o.z, d.x, d.y, d.z, t0s, grow)
                                          : RG_BVH_SCAN;
-        const bool ok = need && cls == RG_BVH_TRAVERSE;
+        // shadow rays of a light with a light buffer: their cell's spheres instead of the walk (near rays)
+        bool lb = false;
+        if (shadow && need && cls == RG_BVH_TRAVERSE && grow == 0.0f && light >= 0 && light < a.n_lbuf)
+            lb = lbuf_spheres(a, src, light, o, d, ld, occl, need);
+        const bool ok = need && cls == RG_BVH_TRAVERSE && !lb;
 #ifdef RG_BVH_STATS
         {
             RG_STAT(8, RG_LANES(need && cls == RG_BVH_SCAN));
@@ -2127,6 +2164,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             hdepth = ohd;
                             pixel = opix;  // error reports name the owner's pixel
                             light_dir_dist(T.lights[oli + 1 + k], hp, sb.d[0], sb.ld[0]);
+                            li = oli + 1 + k;  // the light this helper traces (its li is unused otherwise)
                             mode = MODE_SHADOW_H;
                         }
                     }
@@ -2234,7 +2272,8 @@ void rg_render_kernel(RgKernelArgs a) {
                 // fully counted closest-hit query: in_light = none || dist > light
                 // distance (rendering.rs:150-155), the scene.rs:38 panic iff >= 2 hits, one NaN
                 const bool exact = shadow && (a.nan_scene || ray_exotic(r1.o, r1.d));
-                trace_query<F32F, BVH>(a, src, r1, shadow && !exact, sb.ld[0], c, o1, lane_walk);
+                // li: the light of a shadow ray (owner lanes; fan-out helpers carry the light they trace)
+                trace_query<F32F, BVH>(a, src, r1, shadow && !exact, sb.ld[0], c, o1, lane_walk, shadow ? li : -1);
                 if (exact) {
                     o1 = c.id >= 0 && !(c.t > sb.ld[0]);
                     if (c.nan && c.nhit >= 2) raise_error(a, pixel, RG_ERR_NAN_DISTANCE);

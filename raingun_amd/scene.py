@@ -269,6 +269,14 @@ class DeviceScene:
         """Use (default) or bypass the sphere BVH (include/raingun_debug.h)."""
         _abi.check(_abi.lib().rg_debug_set_bvh(self.handle, 1 if enable else 0))
 
+    def set_lightbuf(self, enable: bool) -> None:
+        """Shadow rays test their light buffer cell's spheres (default) or walk the BVH (include/raingun_debug.h)."""
+        _abi.check(_abi.lib().rg_debug_set_lightbuf(self.handle, 1 if enable else 0))
+
+    def lightbuf_count(self) -> int:
+        """Lights with a shadow-ray light buffer in use (include/raingun_debug.h)."""
+        return int(_abi.lib().rg_debug_lightbuf_count(self.handle))
+
     def set_tile_order(self, mode) -> None:
         """Tile scheduling: True/1 probe-ordered, False/0 raster, -1 auto (include/raingun_debug.h)."""
         _abi.check(_abi.lib().rg_debug_set_tile_order(self.handle, int(mode)))

@@ -26,11 +26,14 @@ def _device():
     assert lib.rg_device_count() > 0, "no HIP device visible"
 
 
-def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0, path=None, bvh=None, lane=None):
+def _compare(oracle_lib, scene, w, h, tile_rows=0, stride=1, offset=0, path=None, bvh=None, lane=None,
+             lightbuf=None):
     desc = SceneDesc(scene)
     ds = DeviceScene(scene, path=path, bvh=bvh)
     if lane is not None:
         ds.set_lane_depth(lane)
+    if lightbuf is not None:
+        ds.set_lightbuf(lightbuf)
     st = _abi.rg_stats()
     g_rgba, g_rgb = ds.render_tiles(w, h, tile_rows, stride, offset, want_rgb=True, stats=st)
     o_st, o_rgba, o_rgb, o_counts, o_err = oracle_lib.render(desc, w, h, tile_rows, stride, offset, want_rgb=True)
@@ -96,6 +99,50 @@ def test_config3_test3_4k(oracle_lib, example_scenes):
 @pytest.mark.parametrize("path,bvh,lane", PATH_BVH)
 def test_synthetic(oracle_lib, n, planes, depth, w, h, path, bvh, lane):
     _compare(oracle_lib, synthetic_scene(n, planes, depth), w, h, path=path, bvh=bvh, lane=lane)
+
+
+@pytest.mark.parametrize("n,planes,depth,w,h", [(16, 2, 5, 320, 240), (1024, 2, 5, 192, 108), (40, 4, 20, 160, 90)])
+@pytest.mark.parametrize("lane", [None, 0])
+def test_synthetic_shadow_rays_walk_the_bvh(oracle_lib, n, planes, depth, w, h, lane):
+    """The heavy path with the shadow-ray light buffers off: every shadow ray walks the BVH
+    (the default path since round 5 tests its cell's spheres instead)."""
+    _compare(oracle_lib, synthetic_scene(n, planes, depth), w, h, path=_abi.PATH_HEAVY, bvh=True, lane=lane,
+             lightbuf=False)
+
+
+def _lights_scene(n=1024):
+    """The synthetic scene plus lights that stress the light buffers: a point light inside the
+    sphere field, one far away, one inside a sphere, an axis-aligned and an oblique directional light."""
+    from raingun_amd.scene import DirectionalLight, SphericalLight
+
+    s = synthetic_scene(n, 2, 5)
+    c0 = s.bodies[2].center  # the first sphere (after the two planes)
+    s.lights += [SphericalLight(position=(0.5, 4.0, -40.0), color=Color(1.0, 0.9, 0.8), intensity=20000.0),
+                 SphericalLight(position=(300.0, 500.0, 200.0), color=Color(0.5, 0.5, 1.0), intensity=9e6),
+                 SphericalLight(position=tuple(c0), color=Color(1.0, 1.0, 1.0), intensity=100.0),
+                 DirectionalLight(direction=(0.0, -1.0, 0.0), color=Color(0.9, 1.0, 0.9), intensity=2.0),
+                 DirectionalLight(direction=(-0.3, -0.2, 1.0), color=Color(1.0, 0.8, 0.8), intensity=2.0)]
+    return s
+
+
+def test_lightbuf_is_built_for_sphere_scenes():
+    ds = DeviceScene(synthetic_scene(1024, 2, 5))
+    assert ds.lightbuf_count() == 3  # 1 directional + 2 spherical lights
+    ds.set_bvh(False)
+    assert ds.lightbuf_count() == 0  # the buffers ride on the BVH's bounds and path
+    ds.close()
+    ds = DeviceScene(_lights_scene())
+    assert ds.lightbuf_count() >= 6
+    ds.close()
+
+
+@pytest.mark.parametrize("lightbuf", [True, False])
+@pytest.mark.parametrize("lane", [None, 0])
+def test_lightbuf_stress_lights(oracle_lib, lightbuf, lane):
+    """Eight lights (inside the sphere field, far away, inside a sphere, axis-aligned and oblique
+    directional) on the 1024-sphere scene: with and without the light buffers, against the CPU
+    restatement."""
+    _compare(oracle_lib, _lights_scene(), 192, 108, path=_abi.PATH_HEAVY, bvh=True, lane=lane, lightbuf=lightbuf)
 
 
 def test_bvh_is_built_for_sphere_scenes():
