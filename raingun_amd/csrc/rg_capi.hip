@@ -223,11 +223,12 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
     a.bvh_margin = s->bvh_margin;
     a.bvh_extent = s->bvh_extent;
     // light buffers only with the BVH (the margins use its bounds; the kernel takes them on the BVH path)
-    const bool lbuf = bvh && s->lbuf_enabled && s->n_lbuf > 0;
+    const bool lbuf = bvh && s->lbuf_enabled && (s->n_lbuf > 0 || s->lb_cam >= 0);
     a.lbuf = lbuf ? s->lbuf : nullptr;
     a.lb_start = lbuf ? s->lb_start : nullptr;
     a.lb_ent = lbuf ? s->lb_ent : nullptr;
     a.n_lbuf = lbuf ? s->n_lbuf : 0;
+    a.lb_cam = lbuf ? s->lb_cam : -1;
     a.bodies = s->bodies;
     a.mats = s->mats;
     a.lights = s->lights;
@@ -557,6 +558,7 @@ void copy_scalars(rg_scene *dst, const rg_scene *src) {
     dst->n_textures = src->n_textures;
     dst->n_nodes = src->n_nodes;
     dst->n_lbuf = src->n_lbuf;
+    dst->lb_cam = src->lb_cam;
     dst->lane_stack = src->lane_stack;
     dst->nan_scene = src->nan_scene;
     dst->bvh_obound = src->bvh_obound;
@@ -791,8 +793,24 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
             h.lbuf[i] = lb.dev;
             ++built;
         }
-        if (!built) h.lbuf.clear();
-        s->n_lbuf = (int32_t)h.lbuf.size();
+        // the camera buffer: a light buffer around the camera (ray.rs:53: every primary ray starts at
+        // the origin), behind the lights' slots; primary rays test their direction's cell
+        const double zero[3] = {0.0, 0.0, 0.0};
+        RgLightBufBuild cam;
+        if (rg_build_lightbuf(sp.data(), (int)h.sph.size(), RG_LIGHT_SPHERICAL, zero, zero, bvh.extent,
+                              (double)bvh.obound, cam)) {
+            const uint32_t ebase = (uint32_t)h.lb_ent.size(), cbase = (uint32_t)h.lb_start.size();
+            for (uint32_t &v : cam.start) v += ebase;
+            cam.dev.cell_off = cbase;
+            cam.dev.always0 += ebase;
+            cam.dev.always1 += ebase;
+            h.lb_start.insert(h.lb_start.end(), cam.start.begin(), cam.start.end());
+            h.lb_ent.insert(h.lb_ent.end(), cam.ent.begin(), cam.ent.end());
+            s->lb_cam = (int32_t)h.lbuf.size();
+            h.lbuf.push_back(cam.dev);
+        }
+        if (!built && s->lb_cam < 0) h.lbuf.clear();
+        s->n_lbuf = built ? (int32_t)nl : 0;
     }
     h.tex_w.resize(d->n_textures);
     h.tex_h.resize(d->n_textures);
@@ -1414,7 +1432,7 @@ rg_status rg_debug_set_lightbuf(rg_scene *s, int32_t enable) {
 int32_t rg_debug_lightbuf_count(const rg_scene *s) {
     if (!s || !s->host || !s->bvh_enabled || s->n_nodes == 0) return 0;
     int32_t n = 0;
-    for (const RgLightBufDev &b : s->host->lbuf) n += b.kind != RG_LB_NONE;
+    for (int32_t i = 0; i < s->n_lbuf; ++i) n += s->host->lbuf[(size_t)i].kind != RG_LB_NONE;
     return n;
 }
 

@@ -700,8 +700,43 @@ __device__ __forceinline__ bool lbuf_spheres(const RgKernelArgs &a, const Src &s
     if (cell >= 0) {
         const uint32_t *st = a.lb_start + B.cell_off + (uint32_t)cell;
         const uint32_t k0 = st[0], k1 = st[1];
-        for (uint32_t k = k0; k < k1 && need; ++k)
-            leaf_query(a, src, (int)a.lb_ent[k], 1, o, d, rf, true, ld, unused, occl, need);
+        // the list's entries four at a time: their loads in flight together, not one round trip per sphere
+        for (uint32_t k = k0; k < k1 && need; k += 4) {
+            uint32_t j[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) j[i] = a.lb_ent[min(k + (uint32_t)i, k1 - 1u)];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (k + (uint32_t)i < k1 && need) leaf_query(a, src, (int)j[i], 1, o, d, rf, true, ld, unused, occl, need);
+        }
+    }
+    return true;
+}
+
+// Primary rays through the camera buffer (a light buffer around the camera at the origin, ray.rs:53:
+// every primary ray starts there): the spheres of the direction's cell and of the always list, each
+// with leaf_primary's f32 pre-filter and exact test, in place of the wave-coherent BVH walk.  The
+// lists hold every sphere the exact test could accept on a ray from the origin in that direction
+// (rg_lightbuf.cpp, spherical case with the light at the camera), and the closest-hit rule is
+// order-independent, so the closest hit is the walk's.  false: not covered (the caller walks).
+template <class Src>
+__device__ __forceinline__ bool cambuf_spheres(const RgKernelArgs &a, const Src &src, V3 d, float dx, float dy, float dz,
+                                               Closest &c) {
+    const RgLightBufDev &B = a.lbuf[a.lb_cam];
+    const int cell = rg_lb_cell(B, 0.0, 0.0, 0.0, d.x, d.y, d.z, a.bvh_obound);
+    if (cell == RG_LB_SKIP) return false;
+    for (uint32_t k = B.always0; k < B.always1; ++k) leaf_primary(a, src, (int)a.lb_ent[k], 1, d, dx, dy, dz, c);
+    if (cell >= 0) {
+        const uint32_t *st = a.lb_start + B.cell_off + (uint32_t)cell;
+        const uint32_t k0 = st[0], k1 = st[1];
+        for (uint32_t k = k0; k < k1; k += 4) {
+            uint32_t j[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) j[i] = a.lb_ent[min(k + (uint32_t)i, k1 - 1u)];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (k + (uint32_t)i < k1) leaf_primary(a, src, (int)j[i], 1, d, dx, dy, dz, c);
+        }
     }
     return true;
 }
@@ -740,7 +775,9 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
             sph_primary<F32F>(a, src, d, c);
             RG_STAT(13, RG_CLOCK() - t0);
         }
-        if (ok) {
+        bool walk = ok;
+        if (ok && a.lb_cam >= 0) walk = !cambuf_spheres(a, src, d, (float)d.x, (float)d.y, (float)d.z, c);
+        if (walk) {
             bool need = true, unused = false;
             bvh_spheres<0>(a, src, o, d, false, 0.0, 0.0, c, unused, need);
         }

@@ -113,6 +113,39 @@ static void check(const Light &l, const double o[3], float obound) {
     }
 }
 
+// camera buffer (a spherical buffer at the origin): a primary ray from the origin along d; the
+// closest hit over the direction's list must equal the brute-force closest hit (t bits, index)
+static long g_cam_rays = 0, g_cam_hits = 0, g_cam_mismatch = 0, g_cam_tests = 0;
+static void check_primary(const RgLightBufBuild &cam, const double d[3], float obound) {
+    const double o[3] = {0.0, 0.0, 0.0};
+    double bt = 0.0, lt = 0.0;
+    int bi = -1, li = -1;
+    auto add = [](double &ct, int &ci, double t, int i) {
+        if (ci < 0 || t < ct || (t == ct && i < ci)) { ct = t; ci = i; }
+    };
+    for (int i = 0; i < n_sph; ++i) {
+        double t;
+        if (sphere_exact(&sp[4 * i], o, d, t)) add(bt, bi, t, i);
+    }
+    ++g_cam_rays;
+    g_cam_hits += bi >= 0;
+    const int cell = rg_lb_cell(cam.dev, 0.0, 0.0, 0.0, d[0], d[1], d[2], obound);
+    if (cell == RG_LB_SKIP) { ++g_skip; return; }
+    auto test = [&](uint32_t j) {
+        double t;
+        ++g_cam_tests;
+        if (sphere_exact(&sp[4 * j], o, d, t)) add(lt, li, t, (int)j);
+    };
+    for (uint32_t k = cam.dev.always0; k < cam.dev.always1; ++k) test(cam.ent[k]);
+    if (cell >= 0)
+        for (uint32_t k = cam.start[cell]; k < cam.start[cell + 1]; ++k) test(cam.ent[k]);
+    if (li != bi || (bi >= 0 && std::memcmp(&lt, &bt, sizeof bt) != 0)) {
+        if (g_cam_mismatch < 5)
+            std::fprintf(stderr, "camera mismatch: d=(%.17g %.17g %.17g) brute %d lb %d\n", d[0], d[1], d[2], bi, li);
+        ++g_cam_mismatch;
+    }
+}
+
 int main(int argc, char **argv) {
     const int R = argc > 1 ? std::atoi(argv[1]) : 4000;
     int n;
@@ -202,10 +235,43 @@ int main(int argc, char **argv) {
             }
         }
     }
-    std::printf("{\"rays\": %ld, \"occluded\": %ld, \"mismatches\": %ld, \"skipped\": %ld, \"empty_cells\": %ld, "
+    // the camera buffer: frustum directions (normalize(sx, sy, -1), ray.rs:46-53), random directions,
+    // and directions grazing a sphere at r (1 +- eps) as seen from the origin
+    RgLightBufBuild cam;
+    const double zero[3] = {0.0, 0.0, 0.0};
+    const bool cam_built = rg_build_lightbuf(sp.data(), n, RG_LIGHT_SPHERICAL, zero, zero, bvh.extent, (double)O, cam);
+    if (cam_built) {
+        for (int r = 0; r < 4 * R; ++r) {
+            double d[3] = {(2.0 * urand() - 1.0) * 1.7778, 2.0 * urand() - 1.0, -1.0};
+            unit(d);
+            check_primary(cam, d, O);
+            rand_dir(d);
+            check_primary(cam, d, O);
+            const double *s = &sp[4 * (int)(urand() * n)];
+            double c[3] = {s[0], s[1], s[2]};
+            const double D = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+            const double rr = std::fabs(s[3]) * (1.0 + (urand() < 0.5 ? -1.0 : 1.0) * (urand() < 0.5 ? 1e-9 : 1e-13));
+            if (D > rr * 1.01) {
+                unit(c);
+                double w[3], u[3];
+                rand_dir(w);
+                cross(c, w, u);
+                unit(u);
+                const double th = std::asin(rr / D);
+                for (int k = 0; k < 3; ++k) d[k] = std::cos(th) * c[k] + std::sin(th) * u[k];
+                unit(d);
+                ++g_near;
+                check_primary(cam, d, O);
+            }
+        }
+    }
+    std::printf("{\"camera_built\": %d, \"camera_rays\": %ld, \"camera_hits\": %ld, \"camera_mismatches\": %ld, "
+                "\"camera_tests_per_ray\": %.3f, ", (int)cam_built, g_cam_rays, g_cam_hits, g_cam_mismatch,
+                g_cam_rays ? (double)g_cam_tests / g_cam_rays : 0.0);
+    std::printf("\"rays\": %ld, \"occluded\": %ld, \"mismatches\": %ld, \"skipped\": %ld, \"empty_cells\": %ld, "
                 "\"grazing\": %ld, \"tests_per_ray\": %.3f, \"lights_built\": %d, \"mean_candidates_max\": %.3f, "
                 "\"max_candidates\": %u, \"brute_tests_per_ray\": %d}\n",
                 g_rays, g_occl, g_mismatch, g_skip, g_empty, g_near, g_rays ? (double)g_tests / g_rays : 0.0, built,
                 mean_c, max_c, n);
-    return g_mismatch ? 1 : 0;
+    return (g_mismatch || g_cam_mismatch) ? 1 : 0;
 }

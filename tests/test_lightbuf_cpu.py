@@ -58,11 +58,12 @@ EXTRA = ((1, (0.5, 4.0, -40.0)), (1, (300.0, 500.0, 200.0)), (0, (0.0, -1.0, 0.0
 def test_lightbuf_matches_brute_force(sim, args):
     rc, res, err = _run(sim, _scene_text(*args, extra_lights=EXTRA))
     assert rc == 0, err
-    assert res["mismatches"] == 0
-    assert res["lights_built"] >= 5
+    assert res["mismatches"] == 0 and res["camera_mismatches"] == 0
+    assert res["lights_built"] >= 5 and res["camera_built"] == 1
+    assert res["camera_hits"] > 1000
     assert res["occluded"] > 1000 and res["grazing"] > 1000 and res["empty_cells"] > 100
     if args[0] >= 1024:  # the point of the structure: few exact tests per shadow ray
-        assert res["tests_per_ray"] < 16
+        assert res["tests_per_ray"] < 16 and res["camera_tests_per_ray"] < 16
 
 
 def test_light_inside_a_sphere(sim):
