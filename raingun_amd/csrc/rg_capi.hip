@@ -257,7 +257,8 @@ RgKernelArgs rg_make_args(const rg_scene *s) {
     a.lds_box = a.lds_dsk + (uint32_t)s->n_dsk * (uint32_t)sizeof(RgDsk);
     a.lds_lights = al16(a.lds_box + (uint32_t)s->n_box * (uint32_t)sizeof(RgBox));
     a.lds_texs = a.lds_lights + (uint32_t)s->n_lights * (uint32_t)sizeof(RgLightDev);
-    a.lds_bodies = al16(a.lds_texs + (uint32_t)s->n_textures * (uint32_t)sizeof(RgTexDev));
+    a.lds_lbuf = al16(a.lds_texs + (uint32_t)s->n_textures * (uint32_t)sizeof(RgTexDev));
+    a.lds_bodies = a.lds_lbuf + (a.lbuf ? (uint32_t)s->n_lbdesc * (uint32_t)sizeof(RgLightBufDev) : 0u);
     a.lds_hot_bytes = a.lds_bodies;
     a.lds_mats = a.lds_bodies + (uint32_t)s->n_bodies * (uint32_t)sizeof(RgBodyDev);
     a.lds_total_bytes = a.lds_mats + (uint32_t)s->n_bodies * (uint32_t)sizeof(RgMatDev);
@@ -533,6 +534,7 @@ const void *lds_blob_for(const rg_scene *s, const RgKernelArgs &a) {
     put(a.lds_mats, h.mats.data(), h.mats.size() * sizeof(RgMatDev));
     put(a.lds_lights, h.lights.data(), h.lights.size() * sizeof(RgLightDev));
     put(a.lds_texs, s->tex_desc.data(), s->tex_desc.size() * sizeof(RgTexDev));
+    if (a.lbuf) put(a.lds_lbuf, h.lbuf.data(), h.lbuf.size() * sizeof(RgLightBufDev));
     void *p = nullptr;
     if (!ok(hipMalloc(&p, img.size()))) { (void)hipGetLastError(); return nullptr; }
     if (!ok(hipMemcpy(p, img.data(), img.size(), hipMemcpyHostToDevice))) { (void)hipFree(p); return nullptr; }
@@ -559,6 +561,7 @@ void copy_scalars(rg_scene *dst, const rg_scene *src) {
     dst->n_nodes = src->n_nodes;
     dst->n_lbuf = src->n_lbuf;
     dst->lb_cam = src->lb_cam;
+    dst->n_lbdesc = src->n_lbdesc;
     dst->lane_stack = src->lane_stack;
     dst->nan_scene = src->nan_scene;
     dst->bvh_obound = src->bvh_obound;
@@ -811,6 +814,7 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         }
         if (!built && s->lb_cam < 0) h.lbuf.clear();
         s->n_lbuf = built ? (int32_t)nl : 0;
+        s->n_lbdesc = (int32_t)h.lbuf.size();
     }
     h.tex_w.resize(d->n_textures);
     h.tex_h.resize(d->n_textures);

@@ -197,6 +197,7 @@ struct RgKernelArgs {
     const uint32_t *lb_ent;    // sphere positions of every list
     int32_t n_lbuf;
     int32_t lb_cam;            // >= 0: lbuf[lb_cam] is the camera buffer (a light buffer at the origin, primary rays)
+    uint32_t lds_lbuf;         // LDS arena: the light-buffer descriptors (hot tables, after the texture descriptors)
 };
 
 __host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }

@@ -168,6 +168,7 @@ struct rg_scene {
     uint32_t *lb_start = nullptr, *lb_ent = nullptr;
     int32_t n_lbuf = 0;             // light slots (the first n_lbuf lights; kind NONE: no buffer)
     int32_t lb_cam = -1;            // the camera buffer's index in lbuf (primary rays), -1: none
+    int32_t n_lbdesc = 0;           // descriptors in lbuf (light slots + the camera buffer)
     bool lbuf_enabled = true;       // rg_debug_set_lightbuf
     float bvh_obound = 0.0f;
     double bvh_rbound = 0.0, bvh_margin = 0.0, bvh_extent = 0.0;

@@ -163,6 +163,8 @@ struct SphScalar {
     const RG_CONST RgDsk *dk;
     const RG_CONST RgBox *bx;
     const RG_CONST RgBvhNode *nd;
+    const RgLightBufDev *lb = nullptr;  // light-buffer descriptors (global)
+    const RgLightDev *lt = nullptr;     // lights (global)
     __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
     __device__ __forceinline__ RgBvhNode getn_uniform(int i) const { return nd[i]; }
     __device__ __forceinline__ RgSph getv(int i) const { return ((const RgSph *)s)[i]; }
@@ -184,6 +186,8 @@ struct SphLds {
     const RgDsk *dk;
     const RgBox *bx;
     const RgBvhNode *nd;
+    const RgLightBufDev *lb = nullptr;  // light-buffer descriptors (LDS copy, hot tables)
+    const RgLightDev *lt = nullptr;     // lights (LDS copy)
     __device__ __forceinline__ RgBvhNode getn_uniform(int i) const { return nd[i]; }
     __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
     __device__ __forceinline__ RgSph getv(int i) const { return s[i]; }
@@ -671,7 +675,7 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             }
         }
     }
-    RG_STAT(12, RG_CLOCK() - t_in);
+    RG_STAT(13, RG_CLOCK() - t_in);  // per-lane walk: word 13 (with the rare full scans)
 }
 
 // Shadow ray of light `light` through the light's buffer (rg_lightbuf_ray.h, rg_lightbuf.cpp):
@@ -682,13 +686,13 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
 template <class Src>
 __device__ __forceinline__ bool lbuf_spheres(const RgKernelArgs &a, const Src &src, int light, V3 o, V3 d, double ld,
                                              bool &occl, bool &need) {
-    const RgLightBufDev &B = a.lbuf[light];
+    const RgLightBufDev &B = src.lb[light];
     if (B.kind == RG_LB_NONE) return false;
     double lx = 0.0, ly = 0.0, lz = 0.0;
     if (B.kind == RG_LB_SPHERICAL) {
-        lx = a.lights[light].v[0];
-        ly = a.lights[light].v[1];
-        lz = a.lights[light].v[2];
+        lx = src.lt[light].v[0];
+        ly = src.lt[light].v[1];
+        lz = src.lt[light].v[2];
     }
     const int cell = rg_lb_cell(B, lx, ly, lz, o.x, o.y, o.z, a.bvh_obound);
     if (cell == RG_LB_SKIP) return false;
@@ -722,7 +726,7 @@ __device__ __forceinline__ bool lbuf_spheres(const RgKernelArgs &a, const Src &s
 template <class Src>
 __device__ __forceinline__ bool cambuf_spheres(const RgKernelArgs &a, const Src &src, V3 d, float dx, float dy, float dz,
                                                Closest &c) {
-    const RgLightBufDev &B = a.lbuf[a.lb_cam];
+    const RgLightBufDev &B = src.lb[a.lb_cam];
     const int cell = rg_lb_cell(B, 0.0, 0.0, 0.0, d.x, d.y, d.z, a.bvh_obound);
     if (cell == RG_LB_SKIP) return false;
     for (uint32_t k = B.always0; k < B.always1; ++k) leaf_primary(a, src, (int)a.lb_ent[k], 1, d, dx, dy, dz, c);
@@ -1523,7 +1527,8 @@ void rg_render_kernel(RgKernelArgs a) {
         stage16(smem + a.lds_dsk, a.dsk, (uint32_t)a.n_dsk * (uint32_t)sizeof(RgDsk));
         stage16(smem + a.lds_box, a.box, a.lds_lights - a.lds_box);
         stage16(smem + a.lds_lights, a.lights, (uint32_t)a.n_lights * (uint32_t)sizeof(RgLightDev));
-        stage16(smem + a.lds_texs, a.texs, a.lds_bodies - a.lds_texs);
+        stage16(smem + a.lds_texs, a.texs, a.lds_lbuf - a.lds_texs);
+        if (a.lbuf) stage16(smem + a.lds_lbuf, a.lbuf, a.lds_bodies - a.lds_lbuf);
         }
         src.f = reinterpret_cast<const RgSphF *>(smem + a.lds_sphf);
         src.f2 = reinterpret_cast<const RgSphF2 *>(smem + a.lds_sphf + (size_t)a.n_sph * sizeof(RgSphF));
@@ -1533,6 +1538,8 @@ void rg_render_kernel(RgKernelArgs a) {
         src.dk = reinterpret_cast<const RgDsk *>(smem + a.lds_dsk);
         src.bx = reinterpret_cast<const RgBox *>(smem + a.lds_box);
         src.nd = reinterpret_cast<const RgBvhNode *>(smem + a.lds_nodes);
+        src.lb = reinterpret_cast<const RgLightBufDev *>(smem + a.lds_lbuf);
+        src.lt = reinterpret_cast<const RgLightDev *>(smem + a.lds_lights);
     } else {
         src.s = rg_cptr(a.sph);
         src.cc = rg_cptr(a.sph_cc);
@@ -1542,6 +1549,8 @@ void rg_render_kernel(RgKernelArgs a) {
         src.dk = rg_cptr(a.dsk);
         src.bx = rg_cptr(a.box);
         src.nd = rg_cptr(a.nodes);
+        src.lb = a.lbuf;
+        src.lt = a.lights;
     }
     if constexpr (LCOLD) {
         if (!blob) {
@@ -2438,7 +2447,7 @@ __global__ __launch_bounds__(256) void rg_trace_kernel(RgKernelArgs a, const dou
     bool occl = false;
     if (alive) {
         SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc), rg_cptr(a.sphf), rg_cptr(a.sphf2),
-                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes)};
+                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes), a.lbuf, a.lights};
         if (a.n_nodes > 0) trace_query<true, true>(a, src, r, false, 0.0, c, occl, a.lane_min_depth <= 1);
         else if (a.path == RG_PATH_HEAVY) trace_query<true, false>(a, src, r, false, 0.0, c, occl);
         else trace_query<false, false>(a, src, r, false, 0.0, c, occl);
@@ -2496,7 +2505,7 @@ __global__ __launch_bounds__(256) void rg_tile_probe_kernel(RgKernelArgs a, uint
         Closest c;
         closest_init(c);
         SphScalar src{rg_cptr(a.sph), rg_cptr(a.sph_cc), rg_cptr(a.sphf), rg_cptr(a.sphf2),
-                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes)};
+                      rg_cptr(a.pln), rg_cptr(a.dsk), rg_cptr(a.box), rg_cptr(a.nodes), a.lbuf, a.lights};
         const double sx = a.prim_sx ? a.prim_sx[x]
                                     : ((((double)x + 0.5) / (double)a.width) * 2.0 - 1.0) * a.aspect * a.fov_adjustment;
         const double sy = a.prim_sy ? a.prim_sy[y] : (1.0 - (((double)y + 0.5) / (double)a.height) * 2.0) * a.fov_adjustment;

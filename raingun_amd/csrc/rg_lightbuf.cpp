@@ -120,7 +120,7 @@ bool build_directional(const double *sp, int n, const double dn[3], double m, Rg
     }
     if (!(std::isfinite(lox) && std::isfinite(hix) && std::isfinite(loy) && std::isfinite(hiy))) return false;
     const double ext = std::max(hix - lox, hiy - loy);
-    const double cs = std::max(0.5 * rsum / n, ext / RG_LB_DIR_MAX_G);
+    const double cs = std::max(RG_LB_DIR_CELL * rsum / n, ext / RG_LB_DIR_MAX_G);
     if (!(cs > 0.0)) return false;
     const float inv = (float)(1.0 / cs);
     // grid origin rounded down to f32; the cells are [g0 + k / inv, g0 + (k + 1) / inv) exactly

@@ -39,6 +39,9 @@ bool rg_build_lightbuf(const double *spheres, int n, int kind, const double dn[3
 #ifndef RG_LB_CUBE_G
 #define RG_LB_CUBE_G 128  // spherical lights: cells per cube-face edge
 #endif
+#ifndef RG_LB_DIR_CELL
+#define RG_LB_DIR_CELL 0.5  // directional lights: cell edge in units of the mean sphere radius
+#endif
 #ifndef RG_LB_DIR_MAX_G
 #define RG_LB_DIR_MAX_G 1024  // directional lights: at most this many cells per grid axis
 #endif

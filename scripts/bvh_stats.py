@@ -3,9 +3,9 @@
 Run with RAINGUN_HIP_LIB pointing at a -DRG_BVH_STATS build
 (scripts/build_variants.sh bvhstats=-DRG_BVH_STATS).  Prints, per ray class
 mix of a 3840x2160 depth-5 frame: wave traversals, node visits and leaf visits
-per traversal, lanes per traversal (coherence), fallback lanes.  With
--DRG_LANE_CLOCK_WORD=13 too, clock_fullscan_frac holds the per-lane walk's wave
-time (the full scans' share is ~0.05 %) and clock_traversal_frac the wave walk's."""
+per traversal, lanes per traversal (coherence), fallback lanes.
+clock_traversal_frac is the wave-coherent walk's share of wave time and
+clock_fullscan_frac the per-lane walk's (with the full scans, ~0.05 %)."""
 import ctypes as C
 import json
 import sys
