@@ -678,76 +678,85 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
     RG_STAT(13, RG_CLOCK() - t_in);  // per-lane walk: word 13 (with the rare full scans)
 }
 
-// Shadow ray of light `light` through the light's buffer (rg_lightbuf_ray.h, rg_lightbuf.cpp):
-// the spheres of the ray's cell and of the light's always list, each with leaf_query's f32
-// pre-filter and exact test, in place of the BVH walk.  The lists hold every sphere the exact
-// test could accept for this ray, so the any-hit answer is the walk's.  false: the buffer does
-// not cover this ray (origin beyond the near-ray bound, no direction), the caller walks the BVH.
+// Light buffers (rg_lightbuf_ray.h, rg_lightbuf.cpp) in two steps, so the list bounds' load is in
+// flight while the plane/disk/box tests run: lbuf_begin finds the ray's cell and loads its list
+// bounds, lbuf_finish tests the list's spheres (and the always list), each with the leaf tests' f32
+// pre-filter and exact test.  The lists hold every sphere the exact test could accept for the ray,
+// so the answer is the BVH walk's; use == false: the buffer does not cover this ray (origin beyond
+// the near-ray bound, no direction) and the caller walks the BVH.
+struct LbRange {
+    uint32_t k0, k1;  // the cell's entries (k0 == k1: an empty cell)
+    bool use;
+};
 template <class Src>
-__device__ __forceinline__ bool lbuf_spheres(const RgKernelArgs &a, const Src &src, int light, V3 o, V3 d, double ld,
-                                             bool &occl, bool &need) {
-    const RgLightBufDev &B = src.lb[light];
-    if (B.kind == RG_LB_NONE) return false;
-    double lx = 0.0, ly = 0.0, lz = 0.0;
-    if (B.kind == RG_LB_SPHERICAL) {
-        lx = src.lt[light].v[0];
-        ly = src.lt[light].v[1];
-        lz = src.lt[light].v[2];
-    }
+__device__ __forceinline__ LbRange lbuf_begin(const RgKernelArgs &a, const Src &src, int buf, V3 o, double lx,
+                                              double ly, double lz) {
+    LbRange r{0u, 0u, false};
+    const RgLightBufDev &B = src.lb[buf];
+    if (B.kind == RG_LB_NONE) return r;
     const int cell = rg_lb_cell(B, lx, ly, lz, o.x, o.y, o.z, a.bvh_obound);
-    if (cell == RG_LB_SKIP) return false;
+    if (cell == RG_LB_SKIP) return r;
+    r.use = true;
+    if (cell >= 0) {
+        const uint32_t *st = a.lb_start + B.cell_off + (uint32_t)cell;
+        r.k0 = st[0];
+        r.k1 = st[1];
+    }
+    return r;
+}
+// the light's position for a spherical light's buffer (directional: unused)
+template <class Src>
+__device__ __forceinline__ V3 lbuf_light_pos(const Src &src, int light) {
+    const RgLightDev &L = src.lt[light];
+    return v3(L.v[0], L.v[1], L.v[2]);
+}
+
+// Shadow ray of `light`: any hit with t <= ld among the listed spheres
+template <class Src>
+__device__ __forceinline__ void lbuf_shadow(const RgKernelArgs &a, const Src &src, int light, const LbRange &r, V3 o,
+                                            V3 d, double ld, bool &occl, bool &need) {
+    const RgLightBufDev &B = src.lb[light];
     const RayF rf = make_rayf(o, d);
     Closest unused;
     closest_init(unused);
     for (uint32_t k = B.always0; k < B.always1 && need; ++k)
         leaf_query(a, src, (int)a.lb_ent[k], 1, o, d, rf, true, ld, unused, occl, need);
-    if (cell >= 0) {
-        const uint32_t *st = a.lb_start + B.cell_off + (uint32_t)cell;
-        const uint32_t k0 = st[0], k1 = st[1];
-        // the list's entries four at a time: their loads in flight together, not one round trip per sphere
-        for (uint32_t k = k0; k < k1 && need; k += 4) {
-            uint32_t j[4];
+    // the list's entries four at a time: their loads in flight together, not one round trip per sphere
+    for (uint32_t k = r.k0; k < r.k1 && need; k += 4) {
+        uint32_t j[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) j[i] = a.lb_ent[min(k + (uint32_t)i, k1 - 1u)];
+        for (int i = 0; i < 4; ++i) j[i] = a.lb_ent[min(k + (uint32_t)i, r.k1 - 1u)];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (k + (uint32_t)i < k1 && need) leaf_query(a, src, (int)j[i], 1, o, d, rf, true, ld, unused, occl, need);
-        }
+        for (int i = 0; i < 4; ++i)
+            if (k + (uint32_t)i < r.k1 && need) leaf_query(a, src, (int)j[i], 1, o, d, rf, true, ld, unused, occl, need);
     }
-    return true;
 }
 
-// Primary rays through the camera buffer (a light buffer around the camera at the origin, ray.rs:53:
-// every primary ray starts there): the spheres of the direction's cell and of the always list, each
-// with leaf_primary's f32 pre-filter and exact test, in place of the wave-coherent BVH walk.  The
-// lists hold every sphere the exact test could accept on a ray from the origin in that direction
-// (rg_lightbuf.cpp, spherical case with the light at the camera), and the closest-hit rule is
-// order-independent, so the closest hit is the walk's.  false: not covered (the caller walks).
+// Primary ray through the camera buffer (a light buffer around the camera at the origin, ray.rs:53:
+// every primary ray starts there; closest hit, order-independent rule)
 template <class Src>
-__device__ __forceinline__ bool cambuf_spheres(const RgKernelArgs &a, const Src &src, V3 d, float dx, float dy, float dz,
-                                               Closest &c) {
+__device__ __forceinline__ void cambuf_primary(const RgKernelArgs &a, const Src &src, const LbRange &r, V3 d, float dx,
+                                               float dy, float dz, Closest &c) {
     const RgLightBufDev &B = src.lb[a.lb_cam];
-    const int cell = rg_lb_cell(B, 0.0, 0.0, 0.0, d.x, d.y, d.z, a.bvh_obound);
-    if (cell == RG_LB_SKIP) return false;
     for (uint32_t k = B.always0; k < B.always1; ++k) leaf_primary(a, src, (int)a.lb_ent[k], 1, d, dx, dy, dz, c);
-    if (cell >= 0) {
-        const uint32_t *st = a.lb_start + B.cell_off + (uint32_t)cell;
-        const uint32_t k0 = st[0], k1 = st[1];
-        for (uint32_t k = k0; k < k1; k += 4) {
-            uint32_t j[4];
+    for (uint32_t k = r.k0; k < r.k1; k += 4) {
+        uint32_t j[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) j[i] = a.lb_ent[min(k + (uint32_t)i, k1 - 1u)];
+        for (int i = 0; i < 4; ++i) j[i] = a.lb_ent[min(k + (uint32_t)i, r.k1 - 1u)];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (k + (uint32_t)i < k1) leaf_primary(a, src, (int)j[i], 1, d, dx, dy, dz, c);
-        }
+        for (int i = 0; i < 4; ++i)
+            if (k + (uint32_t)i < r.k1) leaf_primary(a, src, (int)j[i], 1, d, dx, dy, dz, c);
     }
-    return true;
 }
 
 template <bool F32F, bool BVH, class Src>
 __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &src, V3 d, Closest &c) {
     if constexpr (!BVH) sph_primary<F32F>(a, src, d, c);
+    // the camera buffer's list bounds, loaded while the other bodies are tested
+    [[maybe_unused]] LbRange cam{0u, 0u, false};
+    if constexpr (BVH) {
+        if (a.lb_cam >= 0) cam = lbuf_begin(a, src, a.lb_cam, d, 0.0, 0.0, 0.0);
+    }
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = src.getp(i);
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137
@@ -779,8 +788,8 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
             sph_primary<F32F>(a, src, d, c);
             RG_STAT(13, RG_CLOCK() - t0);
         }
-        bool walk = ok;
-        if (ok && a.lb_cam >= 0) walk = !cambuf_spheres(a, src, d, (float)d.x, (float)d.y, (float)d.z, c);
+        const bool walk = ok && !cam.use;
+        if (ok && cam.use) cambuf_primary(a, src, cam, d, (float)d.x, (float)d.y, (float)d.z, c);
         if (walk) {
             bool need = true, unused = false;
             bvh_spheres<0>(a, src, o, d, false, 0.0, 0.0, c, unused, need);
@@ -800,6 +809,15 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
     bool need = true;
     if constexpr (!BVH) {
         if (!sph_query<F32F>(a, src, o, d, shadow, ld, c, occl, need)) return;
+    }
+    // shadow rays of a light with a buffer: the ray's list bounds, loaded while the planes,
+    // disks and boxes are tested
+    [[maybe_unused]] LbRange lbr{0u, 0u, false};
+    if constexpr (BVH) {
+        if (shadow && light >= 0 && light < a.n_lbuf) {
+            const V3 lp = lbuf_light_pos(src, light);
+            lbr = lbuf_begin(a, src, light, o, lp.x, lp.y, lp.z);
+        }
     }
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = src.getp(i);
@@ -851,9 +869,8 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
                                                            o.x, o.y, o.z, d.x, d.y, d.z, t0s, grow)
                                          : RG_BVH_SCAN;
         // shadow rays of a light with a light buffer: their cell's spheres instead of the walk (near rays)
-        bool lb = false;
-        if (shadow && need && cls == RG_BVH_TRAVERSE && grow == 0.0f && light >= 0 && light < a.n_lbuf)
-            lb = lbuf_spheres(a, src, light, o, d, ld, occl, need);
+        const bool lb = shadow && need && cls == RG_BVH_TRAVERSE && grow == 0.0f && lbr.use;
+        if (lb) lbuf_shadow(a, src, light, lbr, o, d, ld, occl, need);
         const bool ok = need && cls == RG_BVH_TRAVERSE && !lb;
 #ifdef RG_BVH_STATS
         {
