@@ -148,12 +148,16 @@ __device__ __forceinline__ bool disk_hit(const RgDsk &k, V3 o, V3 d, double &t) 
 }
 
 // ---------------------------------------------------------------- sphere sources
-// The sphere tables are read with a wave-uniform index.  Two sources:
+// The sphere tables are read with a wave-uniform index.  Three sources:
 //  * SphLds: the persistent block stages the tables into LDS once and every
 //    test reads them with broadcast ds_read_b128 (always a hit);
 //  * SphScalar: scalar loads through the constant address space (s_load,
-//    SGPR operands) for scenes whose tables exceed the LDS budget.
-struct SphScalar {
+//    SGPR operands) for scenes whose tables exceed the LDS budget;
+//  * SphNodesLds: the same, but the BVH nodes (read per lane by the per-lane
+//    walk: vector loads from global memory otherwise) staged in LDS when the
+//    sphere tables do not fit and the nodes do (BASELINE configs[4]: 4,096 spheres).
+template <bool NODES_LDS>
+struct SphGlobal {
     static constexpr bool in_lds = false;
     const RG_CONST RgSph *s;
     const RG_CONST double *cc;
@@ -162,7 +166,7 @@ struct SphScalar {
     const RG_CONST RgPln *pl;
     const RG_CONST RgDsk *dk;
     const RG_CONST RgBox *bx;
-    const RG_CONST RgBvhNode *nd;
+    typename std::conditional<NODES_LDS, const RgBvhNode *, const RG_CONST RgBvhNode *>::type nd;
     const RgLightBufDev *lb = nullptr;  // light-buffer descriptors (global)
     const RgLightDev *lt = nullptr;     // lights (global)
     __device__ __forceinline__ RgBvhNode getn(int i) const { return nd[i]; }
@@ -176,6 +180,8 @@ struct SphScalar {
     __device__ __forceinline__ RgSphF getf(int i) const { return f[i]; }
     __device__ __forceinline__ RgSphF2 getf2(int i) const { return f2[i]; }
 };
+using SphScalar = SphGlobal<false>;
+using SphNodesLds = SphGlobal<true>;
 struct SphLds {
     static constexpr bool in_lds = true;
     const RgSph *s;
@@ -1489,7 +1495,8 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // (WPS waves per SIMD).  Light path: one-wave blocks, each rendering at most
 // RG_LIGHT_TILES_PER_WAVE tiles (launcher: launch_one).  A block stages the
 // scene into LDS (LSPH: sphere, plane, disk and box tables, lights, texture
-// descriptors; LCOLD: bodies, materials), then every wave repeatedly takes the next 8x8 pixel
+// descriptors; LCOLD: bodies, materials; LCOLD without LSPH: only the BVH nodes, after the per-lane
+// walk stacks -- scenes whose sphere tables exceed the budget), then every wave repeatedly takes the next 8x8 pixel
 // tile from an atomic queue (counters[16..], sharded) and runs the per-lane
 // state machine until its 64 lanes have written their pixels.
 template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0>
@@ -1510,7 +1517,8 @@ void rg_render_kernel(RgKernelArgs a) {
     if (blockIdx.x == 0 && a.counters_next)
         for (uint32_t k = threadIdx.x; k < RG_COUNTER_WORDS; k += blockDim.x) a.counters_next[k] = 0ull;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    typename std::conditional<LSPH, SphLds, SphScalar>::type src;
+    constexpr bool LNODES = !LSPH && LCOLD && BVH;  // only the BVH nodes in LDS (SphNodesLds)
+    typename std::conditional<LSPH, SphLds, typename std::conditional<LNODES, SphNodesLds, SphScalar>::type>::type src;
     Cold T;
     // light path: every one-wave block stages its own copy of the (few-KB) scene; with the
     // arena's device image that is one loop with all its loads in flight at once
@@ -1565,11 +1573,16 @@ void rg_render_kernel(RgKernelArgs a) {
         src.pl = rg_cptr(a.pln);
         src.dk = rg_cptr(a.dsk);
         src.bx = rg_cptr(a.box);
-        src.nd = rg_cptr(a.nodes);
+        if constexpr (LNODES) {  // the nodes after the per-lane walk stacks
+            stage16(smem + a.lds_lstack_bytes, a.nodes, (uint32_t)a.n_nodes * (uint32_t)sizeof(RgBvhNode));
+            src.nd = reinterpret_cast<const RgBvhNode *>(smem + a.lds_lstack_bytes);
+        } else {
+            src.nd = rg_cptr(a.nodes);
+        }
         src.lb = a.lbuf;
         src.lt = a.lights;
     }
-    if constexpr (LCOLD) {
+    if constexpr (LSPH && LCOLD) {
         if (!blob) {
             stage16(smem + a.lds_bodies, a.bodies, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgBodyDev));
             stage16(smem + a.lds_mats, a.mats, (uint32_t)a.n_bodies * (uint32_t)sizeof(RgMatDev));
@@ -2743,6 +2756,11 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
         return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_total_bytes, stream, gt);
     if (a->n_sph > 0 && a->lds_hot_bytes <= budget)
         return launch_one<MAXD, true, false, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_hot_bytes, stream, gt);
+    if constexpr (BVH) {  // the sphere tables do not fit: the BVH nodes alone, after the per-lane walk stacks
+        const uint32_t nodes_lds = a->lds_lstack_bytes + (uint32_t)a->n_nodes * (uint32_t)sizeof(RgBvhNode);
+        if (a->n_nodes > 0 && nodes_lds <= budget)
+            return launch_one<MAXD, false, true, WPS, LB, F32F, BVH, TASKS, TPW>(a, nodes_lds, stream, gt);
+    }
     return launch_one<MAXD, false, false, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_lstack_bytes, stream, gt);
 }
 
