@@ -67,7 +67,7 @@ rg_status rg_debug_set_image_bands(rg_scene *scene, int32_t bands);
 
 /* Tile shape of the one-launch host-visible path: log2 of the tile width,
  * 3 (8x8) .. 6 (64x1), every tile 64 pixels; wider tiles give whole row
- * segments per PCIe write.  0 = automatic (the default: 8x8 for heavy-path
+ * segments per PCIe write.  0 = automatic (the default: 16x4 for heavy-path
  * scenes, 64x1 for light-path scenes).  Device-resident renders always use 8x8. */
 rg_status rg_debug_set_host_tile_shape(rg_scene *scene, int32_t tile_wlog);
 

@@ -40,6 +40,7 @@
 #endif
 
 extern "C" hipError_t rg_launch_render(const RgKernelArgs *a, int maxd, hipStream_t stream);
+extern "C" int rg_host_array_frames(void);
 extern "C" hipError_t rg_render_grid_threads(const RgKernelArgs *a, int maxd, size_t *threads);
 extern "C" int rg_max_array_frames(void);
 extern "C" int rg_launch_global_frames(const RgKernelArgs *a, int maxd);
@@ -315,10 +316,11 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     a.image_rows = image_rows ? 1u : 0u;
     a.pipelined = pipelined ? 1u : 0u;
     const int frames = frames_needed(s->max_depth);
-    // host-frame launches run the MAXD == 0 kernels (the only ones with the
-    // host-frame features: rg_kernels.hip HOSTF), whose frames live in a
-    // global buffer like those of recursion deeper than the compiled arrays
-    const int disp = host_frame ? std::max(frames, rg_max_array_frames() + 1) : frames;
+    // host-frame launches of heavy-path scenes run array-frame kernels with the
+    // host-frame features (rg_kernels.hip HF) up to rg_host_array_frames() frames;
+    // the others the MAXD == 0 kernels, whose frames live in a global buffer
+    const bool host_arrays = frames <= rg_host_array_frames() && rg_heavy_path(a);
+    const int disp = (host_frame && !host_arrays) ? std::max(frames, rg_max_array_frames() + 1) : frames;
     if (rg_launch_global_frames(&a, disp) && out_rows > 0) {
         // frames in a global buffer sized for this launch's (persistent) grid
         size_t threads = 0;

@@ -63,7 +63,11 @@ struct rg_launch_ctx {
 #define RG_HOST_TILE_WLOG_LIGHT 6
 #endif
 #ifndef RG_HOST_TILE_WLOG
-#define RG_HOST_TILE_WLOG 3     // one-launch host-visible frames: 8x8 tiles (RgKernelArgs::tile_wlog)
+// one-launch host-visible frames of heavy-path scenes: 16x4 tiles (RgKernelArgs::tile_wlog) --
+// 64-B row segments per PCIe write, where 8x8 tiles send 32-B ones and 64x1 tiles lose the BVH
+// walk's coherence: north star into pinned memory 2.53 -> 2.14 ms (8x8 -> 16x4; 32x2 2.22,
+// 64x1 2.66: profiles/r05/s13, s14, s15)
+#define RG_HOST_TILE_WLOG 4
 #endif
 #ifndef RG_COPY_HELPERS
 #define RG_COPY_HELPERS 3       // helper threads of the pageable host copy (plus the calling thread)

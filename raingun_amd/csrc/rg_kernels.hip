@@ -1499,8 +1499,9 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // walk stacks -- scenes whose sphere tables exceed the budget), then every wave repeatedly takes the next 8x8 pixel
 // tile from an atomic queue (counters[16..], sharded) and runs the per-lane
 // state machine until its 64 lanes have written their pixels.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0>
-// TPW: light path, tiles per wave (0: RG_LIGHT_TILES_PER_WAVE; < 0: persistent waves that take tiles
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0,
+          bool HF = false>
+// HF: the host-frame features (HOSTF below) with MAXD array frames.  TPW: light path, tiles per wave (0: RG_LIGHT_TILES_PER_WAVE; < 0: persistent waves that take tiles
 // until the queue is empty -- single launches, whose makespan is their slowest wave's tile sum).  Light path (LB > 1): blocks of RG_LIGHT_BLOCK_WAVES waves, at least WPS waves
 // per SIMD (the second bound is waves per execution unit on AMD); heavy path:
 // one block of 4*WPS waves per CU.  Both cap the VGPRs at 512 / WPS.
@@ -1616,7 +1617,7 @@ void rg_render_kernel(RgKernelArgs a) {
     // instantiations, which host-visible one-launch renders use: the array
     // instantiations of device-resident renders stay as lean as before (the
     // runtime checks alone cost test1 3 %, profiles/r02/ab_hostf.txt).
-    constexpr bool HOSTF = MAXD == 0;
+    constexpr bool HOSTF = MAXD == 0 || HF;
     __shared__ uint32_t tile_px[HOSTF ? (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) : 1][64];
     uint32_t *my_px = &tile_px[HOSTF ? threadIdx.x >> 6 : 0][lane];
     // Light path into page-locked host memory without tile publication: the
@@ -2137,7 +2138,7 @@ void rg_render_kernel(RgKernelArgs a) {
             if (tile == 0xFFFFFFFFu) {
                 tiles_left = false;
             } else {
-                constexpr uint32_t kmax = MAXD == 0 || TPW < 0 ? 0u
+                constexpr uint32_t kmax = MAXD == 0 || HF || TPW < 0 ? 0u
                                           : LB > 1 ? (TPW > 0 ? (uint32_t)TPW : RG_LIGHT_TILES_PER_WAVE)
                                                    : RG_HEAVY_TILES_PER_WAVE;
                 if constexpr (kmax > 0) {
@@ -2687,7 +2688,7 @@ static hipError_t occupancy(const void *kern, int threads, size_t lds, int &cus,
 
 // Launch (or, with grid_threads != nullptr, only size: the threads of the
 // grid, which a MAXD == 0 launch needs for its frame buffer) one instantiation.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0>
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0, bool HF = false>
 static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stream, size_t *grid_threads) {
     // Block size.  The heavy path shares one LDS copy of the scene (and the
     // BVH stacks / task pool) among the CU's 4*WPS waves: one block per CU.
@@ -2697,11 +2698,11 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     // waves that finished (a 4*WPS-wave block would keep the CU until its
     // slowest wave -- one refractive tile -- is done).
     constexpr int threads = LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS;  // LB > 1: the light path
-    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH, TASKS, TPW>;
+    auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH, TASKS, TPW, HF>;
     int cus = 0, per_cu = 0;
     const hipError_t oe = occupancy(reinterpret_cast<const void *>(kern), threads, lds, cus, per_cu);
     if (oe != hipSuccess) return oe;
-    if (MAXD == 0 && LB > 1 && per_cu > RG_DEEP_BLOCKS_PER_CU) per_cu = RG_DEEP_BLOCKS_PER_CU;
+    if ((MAXD == 0 || HF) && LB > 1 && per_cu > RG_DEEP_BLOCKS_PER_CU) per_cu = RG_DEEP_BLOCKS_PER_CU;
     // light single launches, persistent waves (TPW < 0): RG_LIGHT_PERSIST_BLOCKS_PER_CU one-wave
     // blocks per CU (2 per SIMD), never more than the occupancy query admits (a scene whose LDS
     // copy allows fewer would otherwise start the extra blocks only after the queue drained)
@@ -2723,7 +2724,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
         if (cap < floor_blocks) cap = floor_blocks;
         if (blocks > cap) blocks = cap;
     }
-    constexpr unsigned long long kmax = MAXD == 0 || TPW < 0 ? 0 : LB > 1 ? (TPW > 0 ? TPW : RG_LIGHT_TILES_PER_WAVE) : RG_HEAVY_TILES_PER_WAVE;
+    constexpr unsigned long long kmax = MAXD == 0 || HF || TPW < 0 ? 0 : LB > 1 ? (TPW > 0 ? TPW : RG_LIGHT_TILES_PER_WAVE) : RG_HEAVY_TILES_PER_WAVE;
     if constexpr (kmax > 0)  // non-persistent: one wave per kmax tiles
         blocks = (tiles + waves * kmax - 1) / (waves * kmax);
     if (a->max_grid_threads && blocks * threads > a->max_grid_threads) blocks = a->max_grid_threads / threads;
@@ -2746,22 +2747,22 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
 #endif
 // RG_HEAVY_SCENE_BODIES and the path decision (rg_heavy_path) live in rg_device.h
 
-template <int MAXD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0>
+template <int MAXD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0, bool HF = false>
 static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t *gt) {
     // the BVH kernels also hold the static per-wave traversal stacks
     constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u) -
-                                (uint32_t)(MAXD != 0 ? 0 : (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) * 64 * 4) -  // tile_px
+                                (uint32_t)(MAXD != 0 && !HF ? 0 : (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) * 64 * 4) -  // tile_px
                                 (TASKS ? (uint32_t)sizeof(TaskPool) : 0u);
     if (a->lds_total_bytes <= budget)  // whole scene (empty sphere part if n_sph == 0)
-        return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_total_bytes, stream, gt);
+        return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS, TPW, HF>(a, a->lds_total_bytes, stream, gt);
     if (a->n_sph > 0 && a->lds_hot_bytes <= budget)
-        return launch_one<MAXD, true, false, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_hot_bytes, stream, gt);
+        return launch_one<MAXD, true, false, WPS, LB, F32F, BVH, TASKS, TPW, HF>(a, a->lds_hot_bytes, stream, gt);
     if constexpr (BVH) {  // the sphere tables do not fit: the BVH nodes alone, after the per-lane walk stacks
         const uint32_t nodes_lds = a->lds_lstack_bytes + (uint32_t)a->n_nodes * (uint32_t)sizeof(RgBvhNode);
         if (a->n_nodes > 0 && nodes_lds <= budget)
-            return launch_one<MAXD, false, true, WPS, LB, F32F, BVH, TASKS, TPW>(a, nodes_lds, stream, gt);
+            return launch_one<MAXD, false, true, WPS, LB, F32F, BVH, TASKS, TPW, HF>(a, nodes_lds, stream, gt);
     }
-    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH, TASKS, TPW>(a, a->lds_lstack_bytes, stream, gt);
+    return launch_one<MAXD, false, false, WPS, LB, F32F, BVH, TASKS, TPW, HF>(a, a->lds_lstack_bytes, stream, gt);
 }
 
 #ifndef RG_LIGHT_BIG_TILES
@@ -2778,7 +2779,7 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 #define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
 #endif
 
-template <int MAXD>
+template <int MAXD, bool HF = false>
 static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t *gt) {
     // Light scenes (few bodies): per-iteration overhead dominates -> fewer,
     // fatter iterations (RG_LB shadow rays per pass) at 2 waves/SIMD.  Heavy
@@ -2787,7 +2788,8 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
     const bool heavy = rg_heavy_path(*a);
 #ifndef RG_DEV_HEAVY_ONLY  // development builds: resource reports of the heavy kernels only
     if (!heavy) {
-        if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT) {
+        if constexpr (HF) return hipErrorInvalidValue;  // light host frames: the MAXD == 0 kernels
+        if constexpr (MAXD != 0 && !HF && RG_LIGHT_SINGLE_PERSISTENT) {
             // a launch on its own (not one of several frames in flight): persistent waves at full
             // occupancy balance the tiles dynamically, where a fixed tiles-per-wave grid makes every
             // wave render exactly that many tiles and the slowest wave's sum the makespan
@@ -2795,7 +2797,7 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
             if (!a->pipelined && (RG_LIGHT_SINGLE_PERSISTENT != 2 || rg_tile_count(*a) < RG_LIGHT_BIG_TILES))
                 return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, -1>(a, stream, gt);
         }
-        return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false>(a, stream, gt);
+        return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, 0, HF>(a, stream, gt);
     }
 #endif
 #ifdef RG_DEV_LIGHT_ONLY  // development builds: resource reports of the light kernels only
@@ -2807,16 +2809,31 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
     // profiles/r02/ab_task_split.txt); a single small launch keeps it (its latency)
     const bool tasks = RG_HEAVY_TASKS && tiles < RG_HEAVY_TASK_TILES && !a->pipelined;
     if (a->n_nodes > 0)
-        return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, true>(a, stream, gt)
-                     : launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, false>(a, stream, gt);
-    return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, true>(a, stream, gt)
-                 : launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, false>(a, stream, gt);
+        return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, true, 0, HF>(a, stream, gt)
+                     : launch_waves<MAXD, RG_HEAVY_WPS, 1, true, true, false, 0, HF>(a, stream, gt);
+    return tasks ? launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, true, 0, HF>(a, stream, gt)
+                 : launch_waves<MAXD, RG_HEAVY_WPS, 1, RG_HEAVY_F32_FILTER, false, false, 0, HF>(a, stream, gt);
 #endif
 }
 
 // Frame-stack capacity of each compiled array instantiation; deeper scenes use
 // the global frame buffer (MAXD == 0).
 extern "C" int rg_max_array_frames(void) { return 64; }
+
+// Host-frame launches (pixels into page-locked host memory, tile publication,
+// cancellation, other tile shapes) of heavy-path scenes needing at most this
+// many frames run array-frame kernels with the host-frame features (HF:
+// north star into pinned memory 2.59 -> 2.53 ms, profiles/r05/s15); deeper
+// ones and light-path scenes the MAXD == 0 kernels (light HF measured slower:
+// test1 0.878 -> 0.895 ms, 9 spills).
+#ifndef RG_HOST_ARRAY_FRAMES
+#define RG_HOST_ARRAY_FRAMES 8
+#endif
+extern "C" int rg_host_array_frames(void) { return RG_HOST_ARRAY_FRAMES; }
+
+static bool host_frame_launch(const RgKernelArgs *a) {
+    return a->defer_px || a->tile_flags || a->cancel || a->image_rows || a->tile_wlog != 3u;
+}
 
 // Does this launch keep its frames in the launch context's global buffer (the
 // host sizes it with rg_render_grid_threads)?  Depths above the arrays.
@@ -2826,6 +2843,15 @@ extern "C" int rg_launch_global_frames(const RgKernelArgs *a, int maxd) {
 }
 
 static hipError_t dispatch_depth(const RgKernelArgs *a, int maxd, hipStream_t stream, size_t *gt) {
+    if (host_frame_launch(a)) {
+        if (RG_HOST_ARRAY_FRAMES > 0 && maxd <= RG_HOST_ARRAY_FRAMES && rg_heavy_path(*a))
+            return launch_depth<8, true>(a, stream, gt);
+#ifdef RG_DEV_ONE_DEPTH
+        return hipErrorNotSupported;
+#else
+        return launch_depth<0>(a, stream, gt);
+#endif
+    }
 #ifdef RG_DEV_ONE_DEPTH  // development builds: the MAXD = 8 instantiations only
     return maxd <= 8 ? launch_depth<8>(a, stream, gt) : hipErrorNotSupported;
 #else

@@ -298,7 +298,7 @@ class DeviceScene:
 
     def set_host_tile_shape(self, tile_wlog: int) -> None:
         """Tile shape of one-launch host-visible renders: log2 of the tile width, 3 (8x8) .. 6 (64x1);
-        0 = automatic (8x8 for heavy-path scenes, 64x1 for light-path scenes)."""
+        0 = automatic (16x4 for heavy-path scenes, 64x1 for light-path scenes)."""
         _abi.check(_abi.lib().rg_debug_set_host_tile_shape(self.handle, int(tile_wlog)))
 
     def bvh_info(self) -> _abi.rg_bvh_info:

@@ -2,8 +2,10 @@
 """Host-visible rg_render_image: ms per 4K frame against the host path
 setting, into a page-locked and a pageable buffer.  A setting is `bands`
 (rg_debug_set_image_bands: 0 automatic, -1 one launch writing host memory,
-k row bands) or `-1:<tile_wlog>` (one launch with that tile shape).
-  python scripts/hv_sweep.py [--workload test1|synth1024] [setting ...]"""
+k row bands), `-1:<tile_wlog>` (one launch with that tile shape; 0 automatic)
+or `-1:<tile_wlog>:<tile order>` (rg_debug_set_tile_order: -1 automatic,
+0 raster, 1 cost-ordered).
+  python scripts/hv_sweep.py [--workload test1|synth1024] [--pinned] [setting ...]"""
 import json
 import sys
 import time
@@ -28,15 +30,20 @@ def main():
     ds = DeviceScene(scene, device=0)
     lib = _abi.lib()
     ref = ds.render_image(W, H)
+    kinds = ("pinned", "pageable")
+    if args[:1] == ["--pinned"]:
+        kinds, args = ("pinned",), args[1:]
     settings = args or ["0", "-1:6", "-1:5", "-1:3", "3"]
-    for kind in ("pinned", "pageable"):
+    for kind in kinds:
         buf = np.empty((H, W, 4), dtype=np.uint8)
         reg = _abi.HostRegistration(buf) if kind == "pinned" else None
         for setting in settings:
-            k, _, shape = setting.partition(":")
+            k, _, rest = setting.partition(":")
+            shape, _, order = rest.partition(":")
             k = int(k)
+            ds.set_tile_order(int(order) if order else -1)
             _abi.check(lib.rg_debug_set_image_bands(ds.handle, k))
-            if shape:
+            if shape and int(shape):
                 ds.set_host_tile_shape(int(shape))
             else:  # the automatic shape (libraries before round 3's tile ring reject 0: their default is 8x8)
                 lib.rg_debug_set_host_tile_shape(ds.handle, 0)
