@@ -266,6 +266,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     ds = DeviceScene(scene, device=local_rank)  # scene + textures uploaded once, resident in HBM
     if args.tile_order >= 0:
         ds.set_tile_order(args.tile_order)
+    if args.lane_depth is not None:
+        ds.set_lane_depth(args.lane_depth)
     lib = _abi.lib()
     bvh = ds.bvh_info()
 
@@ -646,6 +648,8 @@ def main() -> None:
                          "faster than with 16, profiles/r01/bench_rank_shares.txt)")
     ap.add_argument("--share-rank", type=int, default=0, help="diagnostic: which rank's share --share times")
     ap.add_argument("--depth", type=int, default=None, help="diagnostic: override the workload's recursion depth")
+    ap.add_argument("--lane-depth", type=int, default=None,
+                    help="diagnostic: rays at recursion depth >= this walk the BVH per lane (rg_debug_set_lane_depth)")
     ap.add_argument("--tile-order", type=int, default=-1,
                     help="diagnostic: 1 = probe-ordered tiles, 0 = raster order, -1 = library default")
     ap.add_argument("--share", type=int, default=1,

@@ -21,6 +21,7 @@ for name, (n, planes, depth, w, h) in {"synth1024_4k_d5": (1024, 2, 5, 3840, 216
                                       "synth4096p8_1080p_d8": (4096, 8, 8, 1920, 1080)}.items():
     ds = DeviceScene(synthetic_scene(n, planes, depth))
     st = _abi.rg_stats()
+    ds.set_image_bands(1)  # one launch: rg_debug_counters reads the last launch's words
     ds.render_tiles(w, h, stats=st)
     c = (C.c_uint64 * 16)()
     _abi.check(_abi.lib().rg_debug_counters(ds.handle, c))
