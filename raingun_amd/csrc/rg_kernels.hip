@@ -1326,7 +1326,8 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 // across the waves of a CU.  Waits only ever point down a tree, so there is
 // no cycle: every awaited subtree is held by a live lane.
 #ifndef RG_PIPE_TILES_PER_WAVE
-#define RG_PIPE_TILES_PER_WAVE 32  // heavy launches with frames in flight (launch_one, RgKernelArgs::pipelined)
+#define RG_PIPE_TILES_PER_WAVE 64  // heavy launches with frames in flight (launch_one, RgKernelArgs::pipelined;
+                                   // 32 -> 64: configs[4] scene at 1080p 2.50 -> 2.33 ms, profiles/r05/s21)
 #endif
 #ifndef RG_PIPE_MIN_CU_DIV
 #define RG_PIPE_MIN_CU_DIV 4  // ... and at least 1/this of the CUs' blocks (3 -> 4: north-star 1/8 share 0.349 -> 0.327 ms)
@@ -1345,7 +1346,11 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v32) {
 #define RG_HEAVY_TILES_PER_WAVE 0  // heavy path: 0 = persistent blocks (one per CU)
 #endif
 #ifndef RG_SHADOW_FAN
-#define RG_SHADOW_FAN 3   // heavy path: up to this many more lights of a hit traced by idle lanes per iteration
+// heavy path, single small launches (TASKS): up to this many more lights of a hit traced by idle
+// lanes per iteration.  Off for frames in flight and whole frames since the light buffers made
+// shadow rays cheap: north star 1.594 -> 1.497 ms (8K 5.38 -> 5.06), while a 1/8 share as one
+// launch keeps it (slowest share 0.648 vs 0.712 ms without; profiles/r05/s20, s21)
+#define RG_SHADOW_FAN 3
 #endif
 __device__ __forceinline__ double readlane_d(double v, int l) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -1717,7 +1722,7 @@ void rg_render_kernel(RgKernelArgs a) {
     uint32_t tile_iters = 0;
 #endif
     for (;;) {
-        if constexpr (LB == 1 && RG_SHADOW_FAN > 0) {
+        if constexpr (LB == 1 && TASKS && RG_SHADOW_FAN > 0) {
             // shadow fan-out, collect: the helpers' occlusion bits (every lane active here)
             if (__any(nfan > 0)) {
                 fan_bits = 0u;
@@ -1929,7 +1934,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             fin = cadd(fin, cmul(bcol, lc));
                         }
                     }
-                    if constexpr (LB == 1 && RG_SHADOW_FAN > 0) {
+                    if constexpr (LB == 1 && TASKS && RG_SHADOW_FAN > 0) {
                         // the lights helper lanes traced, in light order (rendering.rs:141-170)
                         for (int k = 0; k < nfan; ++k) {
                             const RgLightDev L = T.lights[li + 1 + k];
@@ -2210,7 +2215,7 @@ void rg_render_kernel(RgKernelArgs a) {
                 continue;
             }
         }
-        if constexpr (LB == 1 && RG_SHADOW_FAN > 0) {
+        if constexpr (LB == 1 && TASKS && RG_SHADOW_FAN > 0) {
             // shadow fan-out, assign: a lane about to trace the shadow ray of light li
             // hands lights li+1.. of the same hit to idle lanes of its wave, so up to
             // 1 + RG_SHADOW_FAN shadow rays of a hit are traced in one iteration instead
@@ -2788,16 +2793,19 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
     const bool heavy = rg_heavy_path(*a);
 #ifndef RG_DEV_HEAVY_ONLY  // development builds: resource reports of the heavy kernels only
     if (!heavy) {
-        if constexpr (HF) return hipErrorInvalidValue;  // light host frames: the MAXD == 0 kernels
-        if constexpr (MAXD != 0 && !HF && RG_LIGHT_SINGLE_PERSISTENT) {
-            // a launch on its own (not one of several frames in flight): persistent waves at full
-            // occupancy balance the tiles dynamically, where a fixed tiles-per-wave grid makes every
-            // wave render exactly that many tiles and the slowest wave's sum the makespan
-            // (2: launches below RG_LIGHT_BIG_TILES tiles only -- rg_render_multi's shares and bands)
-            if (!a->pipelined && (RG_LIGHT_SINGLE_PERSISTENT != 2 || rg_tile_count(*a) < RG_LIGHT_BIG_TILES))
-                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, -1>(a, stream, gt);
+        if constexpr (HF) {
+            return hipErrorInvalidValue;  // light host frames run the MAXD == 0 kernels
+        } else {
+            if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT) {
+                // a launch on its own (not one of several frames in flight): persistent waves at full
+                // occupancy balance the tiles dynamically, where a fixed tiles-per-wave grid makes every
+                // wave render exactly that many tiles and the slowest wave's sum the makespan
+                // (2: launches below RG_LIGHT_BIG_TILES tiles only -- rg_render_multi's shares and bands)
+                if (!a->pipelined && (RG_LIGHT_SINGLE_PERSISTENT != 2 || rg_tile_count(*a) < RG_LIGHT_BIG_TILES))
+                    return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, -1>(a, stream, gt);
+            }
+            return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false>(a, stream, gt);
         }
-        return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, 0, HF>(a, stream, gt);
     }
 #endif
 #ifdef RG_DEV_LIGHT_ONLY  // development builds: resource reports of the light kernels only

@@ -4,7 +4,8 @@
 
 Compiles rg_kernels.hip with the library's flags and -Rpass-analysis=kernel-resource-usage
 and prints VGPRs, spilled VGPRs, scratch bytes per lane, occupancy and static LDS for the
-MAXD = 8 instantiations (the ones the bench configurations run)."""
+MAXD = 8 instantiations (the ones the bench configurations run; "host": the
+host-frame ones, "tpw=-1": the light path's persistent single launches)."""
 import re
 import subprocess
 import sys
@@ -29,10 +30,15 @@ for line in out.stderr.splitlines():
     if m and cur is not None:
         cur[m.group(1)] = int(m.group(2))
 for r in rows:
-    m = re.match(r"_Z16rg_render_kernelILi(\d+)ELb(\d)ELb(\d)ELi(\d+)ELi(\d+)ELb(\d)ELb(\d)ELb(\d)E", r["name"])
+    m = re.match(r"_Z16rg_render_kernelILi(\d+)ELb(\d)ELb(\d)ELi(\d+)ELi(\d+)ELb(\d)ELb(\d)ELb(\d)ELi(n?\d+)ELb(\d)E",
+                 r["name"])
     if not m or m.group(1) != "8":
         continue
-    maxd, lsph, lcold, wps, lb, f32f, bvh, tasks = m.groups()
+    maxd, lsph, lcold, wps, lb, f32f, bvh, tasks, tpw, hf = m.groups()
     kind = "light" if int(lb) > 1 else "heavy"
-    print(f"{kind:5s} <{maxd},{lsph},{lcold},{wps},{lb},{f32f},{bvh},{tasks}>  VGPRs {r.get('VGPRs')}  spill {r.get('VGPRs Spill')}"
+    if tpw != "0":
+        kind += f" tpw={tpw.replace('n', '-')}"
+    if hf == "1":
+        kind += " host"
+    print(f"{kind:12s} <{maxd},{lsph},{lcold},{wps},{lb},{f32f},{bvh},{tasks}>  VGPRs {r.get('VGPRs')}  spill {r.get('VGPRs Spill')}"
           f"  scratch {r.get('ScratchSize [bytes/lane]')} B/lane  occ {r.get('Occupancy [waves/SIMD]')}  lds {r.get('LDS Size [bytes/block]')}")
