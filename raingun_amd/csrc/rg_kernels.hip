@@ -2108,8 +2108,11 @@ void rg_render_kernel(RgKernelArgs a) {
             // previous tile's start, so the atomic's round trip overlaps that tile (round 4, same
             // box, interleaved: test1 0.2972 -> 0.2939 ms over 200 frames, test3 0.2656 -> 0.2631:
             // profiles/r04/s21/session.txt, s22).  Not on the heavy path: a claimed tile waits
-            // behind the wave's current (long) one, which lengthens the tail (north star +0.6 %)
-            if constexpr (!HOSTF && LB > 1) {
+            // behind the wave's current (long) one, which lengthens the tail (north star +0.6 %);
+            // nor in the light path's persistent single launches (TPW < 0), for the same reason:
+            // rg_render_multi's shares, whose waves ended by 84 us (p50) while claimed tiles still
+            // started at 145 us (profiles/r05/s18, s26)
+            if constexpr (!HOSTF && LB > 1 && TPW >= 0) {
                 if (pf_valid) {  // the slot claimed at the previous tile's start
                     const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)pf_k, 0, 64));
                     const unsigned long long t = (unsigned long long)k * RG_NQ + qi;
@@ -2151,7 +2154,7 @@ void rg_render_kernel(RgKernelArgs a) {
                     // drains through the hardware dispatcher wave (block) by wave
                     if (++tiles_taken >= kmax) tiles_left = false;
                 }
-                if constexpr (!HOSTF && LB > 1) {
+                if constexpr (!HOSTF && LB > 1 && TPW >= 0) {
                     // claim the wave's NEXT queue slot now: the atomic's round trip overlaps this
                     // tile's work instead of stalling the wave between tiles (the wave renders
                     // the claimed tile, or finds the head drained, at its next tile start)
