@@ -7,7 +7,7 @@ HIP events on its stream) of the whole frame and of every rank's 1/8 share
 8-device rg_render_multi rehearsal (each device's timeline alone, bench.py's
 multi_rehearsal).  RAINGUN_HIP_LIB selects a variant library.
 
-    python scripts/latency_probe.py [--no-multi] [--tile-order] [workload ...]   -> JSON on stdout
+    python scripts/latency_probe.py [--no-multi] [--tile-order] [--lane-depth=N] [workload ...]   -> JSON on stdout
 """
 import ctypes as C
 import json
@@ -44,13 +44,15 @@ def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     multi = "--no-multi" not in sys.argv
     order = 1 if "--tile-order" in sys.argv else -1  # --tile-order: probe-ordered tiles on every path
+    lane_depth = next((int(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--lane-depth=")), -1)
     lib = _abi.lib()
     out = {"lib": str(getattr(lib, "_name", "")), "width": W, "height": H}
     for wl in args or ["test1", "synth1024"]:
         scene = bench.load_workload(wl, W, H)[0]
         ds = DeviceScene(scene)
         ds.set_tile_order(order)
-        r = {"tile_order": order}
+        ds.set_lane_depth(lane_depth)
+        r = {"tile_order": order, "lane_depth": lane_depth}
         r["whole_kernel_ms"], rays = share_ms(ds, lib, 1, 0)
         per = [share_ms(ds, lib, N, k) for k in range(N)]
         r["share8_kernel_ms"] = [round(p[0], 4) for p in per]
