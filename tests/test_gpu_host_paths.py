@@ -63,6 +63,35 @@ def test_render_image_host_visible(oracle_lib, example_scenes, kind, w, h, bands
         ds.close()
 
 
+@pytest.mark.parametrize("depth", [5, 8, 9, 66])  # <= 8 frames: array-frame host kernels (HF); deeper: MAXD == 0
+@pytest.mark.parametrize("bands", [-1, 0])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_heavy_host_frames_by_depth(oracle_lib, depth, bands, pinned):
+    """Host-visible frames of a heavy-path (BVH) scene on both host-frame kernel
+    families: scenes needing at most 8 frames run the MAXD = 8 array-frame kernels
+    with the host-frame features, deeper ones the MAXD = 0 kernels (rg_kernels.hip
+    dispatch_depth); the automatic 16x4 host tiles in both."""
+    scene = synthetic_scene(200, 2, 5) if depth <= 9 else _mirror_corridor(depth)
+    scene.max_recursion_depth = depth
+    w, h = 160, 90
+    o_st, o_rgba, _, o_counts, _ = _oracle(oracle_lib, scene, w, h)
+    assert o_st == 0
+    ds = DeviceScene(scene, path=_abi.PATH_HEAVY)
+    ds.set_image_bands(bands)
+    out = np.full((h, w, 4), 77, dtype=np.uint8)
+    reg = _abi.HostRegistration(out) if pinned else None
+    try:
+        for _ in range(2):
+            st = _abi.rg_stats()
+            got = ds.render_image(w, h, stats=st, out=out)
+            assert np.array_equal(got, o_rgba)
+            assert st.rays.as_dict() == o_counts
+    finally:
+        if reg is not None:
+            reg.close()
+        ds.close()
+
+
 @pytest.mark.parametrize("wlog", [0, 3, 4, 5, 6])  # 0: the automatic shape
 @pytest.mark.parametrize("kind,w,h", [("test1", 321, 243), ("synth200", 200, 111), ("test3", 97, 61)])
 def test_host_tile_shapes(oracle_lib, example_scenes, kind, w, h, wlog):
