@@ -65,6 +65,12 @@ rg_status rg_debug_set_tile_order(rg_scene *scene, int32_t mode);
  * (~2 Mpx each, at most 3).  Results are identical for every value. */
 rg_status rg_debug_set_image_bands(rg_scene *scene, int32_t bands);
 
+/* bands = -2 (page-locked whole-frame renders; otherwise as -1): the frame in two
+ * concurrent parts sharing the PCIe link -- the top `pct` percent of the rows
+ * rendered into device memory and copied by DMA, the rest in one launch writing
+ * host memory.  pct 1..99, 0 = the library default.  Results are identical. */
+rg_status rg_debug_set_host_split(rg_scene *scene, int32_t pct);
+
 /* Tile shape of the one-launch host-visible path: log2 of the tile width,
  * 3 (8x8) .. 6 (64x1), every tile 64 pixels; wider tiles give whole row
  * segments per PCIe write.  0 = automatic (the default: 16x4 for heavy-path

@@ -140,7 +140,7 @@ EXPORTED_SYMBOLS = (
 # include/raingun_debug.h
 DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
                  "rg_debug_set_lightbuf", "rg_debug_lightbuf_count",
-                 "rg_debug_set_tile_order", "rg_debug_set_lane_depth", "rg_debug_set_image_bands",
+                 "rg_debug_set_tile_order", "rg_debug_set_lane_depth", "rg_debug_set_image_bands", "rg_debug_set_host_split",
                  "rg_debug_set_host_tile_shape", "rg_debug_set_multi", "rg_debug_gather_noop")
 # include/raingun_frames.h
 FRAMES_SYMBOLS = ("rg_frames_create", "rg_frames_destroy", "rg_frames_step", "rg_frames_flush", "rg_frames_image",
@@ -207,6 +207,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_set_lane_depth.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_set_image_bands.restype = C.c_int32
     lib.rg_debug_set_image_bands.argtypes = [C.c_void_p, C.c_int32]
+    lib.rg_debug_set_host_split.restype = C.c_int32
+    lib.rg_debug_set_host_split.argtypes = [C.c_void_p, C.c_int32]
     if hasattr(lib, "rg_debug_set_multi"):  # absent from pre-round-3 builds
         lib.rg_debug_set_multi.restype = C.c_int32
         lib.rg_debug_set_multi.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32]

@@ -178,7 +178,8 @@ struct rg_scene {
     double bvh_rbound = 0.0, bvh_margin = 0.0, bvh_extent = 0.0;
     rg_bvh_info bvh_info{};
     int tile_order = -1;  // expensive tiles first (rg_kernels.hip "tile ordering"): -1 auto (heavy path), 0, 1
-    int image_bands = 0;  // host-visible frames: 0 auto, -1 one launch writing host memory, 1..16 row bands
+    int image_bands = 0;  // host-visible frames: 0 auto, -1 one launch writing host memory, -2 split, 1..16 row bands
+    int host_split_pct = 0;  // -2 (split): percent of the frame's rows rendered into device memory + DMA (0: default)
     int host_tile_wlog = RG_HOST_TILE_WLOG;  // tile shape of the one-launch host-visible path
     bool host_tile_forced = false;           // set by rg_debug_set_host_tile_shape (else light scenes: 64x1)
     // rg_render_multi (rg_debug_set_multi): 0 each device copies its rows to the host, 1 RCCL gather;

@@ -296,6 +296,11 @@ class DeviceScene:
         _abi.check(_abi.lib().rg_debug_set_multi(self.handle, int(mode), 1 if stand_in else 0, int(bands),
                                                  int(only_rank)))
 
+    def set_host_split(self, pct: int) -> None:
+        """Image bands -2 (split host frames): percent of the rows rendered into device
+        memory and copied by DMA beside the one-launch rest; 0 = default (raingun_debug.h)."""
+        _abi.check(_abi.lib().rg_debug_set_host_split(self.handle, int(pct)))
+
     def set_host_tile_shape(self, tile_wlog: int) -> None:
         """Tile shape of one-launch host-visible renders: log2 of the tile width, 3 (8x8) .. 6 (64x1);
         0 = automatic (16x4 for heavy-path scenes, 64x1 for light-path scenes)."""

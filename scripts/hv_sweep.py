@@ -4,7 +4,8 @@ setting, into a page-locked and a pageable buffer.  A setting is `bands`
 (rg_debug_set_image_bands: 0 automatic, -1 one launch writing host memory,
 k row bands), `-1:<tile_wlog>` (one launch with that tile shape; 0 automatic)
 or `-1:<tile_wlog>:<tile order>` (rg_debug_set_tile_order: -1 automatic,
-0 raster, 1 cost-ordered).
+0 raster, 1 cost-ordered); `-2:0:-1:<pct>`: split frames with pct percent of
+the rows rendered into device memory and copied by DMA.
   python scripts/hv_sweep.py [--workload test1|synth1024] [--pinned] [setting ...]"""
 import json
 import sys
@@ -39,9 +40,12 @@ def main():
         reg = _abi.HostRegistration(buf) if kind == "pinned" else None
         for setting in settings:
             k, _, rest = setting.partition(":")
-            shape, _, order = rest.partition(":")
+            shape, _, rest = rest.partition(":")
+            order, _, pct = rest.partition(":")
             k = int(k)
             ds.set_tile_order(int(order) if order else -1)
+            if hasattr(_abi.lib(), "rg_debug_set_host_split"):
+                ds.set_host_split(int(pct) if pct else 0)
             _abi.check(lib.rg_debug_set_image_bands(ds.handle, k))
             if shape and int(shape):
                 ds.set_host_tile_shape(int(shape))

@@ -38,7 +38,7 @@ def _oracle(oracle_lib, scene, w, h):
 
 
 # ---------------------------------------------------------------- host-visible frames
-@pytest.mark.parametrize("bands", [-1, 0, 1, 3, 7])  # -1: one launch writing host memory; 0: automatic
+@pytest.mark.parametrize("bands", [-2, -1, 0, 1, 3, 7])  # -1: one launch writing host memory; -2 split; 0: automatic
 @pytest.mark.parametrize("kind,w,h", [("test1", 800, 600), ("synth200", 640, 360), ("test2", 97, 61),
                                       ("test3", 33, 9)])
 @pytest.mark.parametrize("pinned", [False, True])
@@ -64,7 +64,7 @@ def test_render_image_host_visible(oracle_lib, example_scenes, kind, w, h, bands
 
 
 @pytest.mark.parametrize("depth", [5, 8, 9, 66])  # <= 8 frames: array-frame host kernels (HF); deeper: MAXD == 0
-@pytest.mark.parametrize("bands", [-1, 0])
+@pytest.mark.parametrize("bands", [-2, -1, 0])
 @pytest.mark.parametrize("pinned", [False, True])
 def test_heavy_host_frames_by_depth(oracle_lib, depth, bands, pinned):
     """Host-visible frames of a heavy-path (BVH) scene on both host-frame kernel
