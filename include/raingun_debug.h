@@ -60,9 +60,10 @@ rg_status rg_debug_set_tile_order(rg_scene *scene, int32_t mode);
  * host memory (the caller's, or a pinned frame copied band by band into a
  * pageable caller buffer as the kernel publishes finished tiles);
  * 1..16 = render in this many row bands into device memory, each band's
- * device-to-host copy overlapping the next bands' renders; 0 (default) =
- * one launch for heavy-path scenes into page-locked buffers, else bands
- * (~2 Mpx each, at most 3).  Results are identical for every value. */
+ * device-to-host copy overlapping the next bands' renders; -2 = split (below);
+ * 0 (default) = into page-locked buffers: split for light-path scenes, one
+ * launch for heavy-path scenes; into pageable buffers: bands (~2 Mpx each, at
+ * most 3).  Results are identical for every value. */
 rg_status rg_debug_set_image_bands(rg_scene *scene, int32_t bands);
 
 /* bands = -2 (page-locked whole-frame renders; otherwise as -1): the frame in two

@@ -1180,11 +1180,16 @@ rg_status render_host_direct(const rg_scene *s, uint32_t W, uint32_t H, const rg
 // the rest is ONE launch writing its pixels over PCIe itself
 // (render_host_direct's kernel).  The one-launch kernel alone reaches ~38 GB/s
 // of the ~55 GB/s a copy does; the copy of the first part runs beside it.
+// The automatic choice for light-path scenes into page-locked buffers (test1
+// 4K 0.90 -> 0.80 ms, test3 0.835 -> 0.80: profiles/r05/s31, s32); heavy
+// scenes keep the one launch (north star 2.13 -> 2.23-2.70 ms split).
 #ifndef RG_HOST_SPLIT_PCT
 #define RG_HOST_SPLIT_PCT 35
 #endif
 #ifndef RG_HOST_SPLIT_B_FIRST
-#define RG_HOST_SPLIT_B_FIRST 0
+// part B's persistent host-frame launch first, part A's beside it: B's PCIe writes start at once
+// (test1 4K pinned 0.854 -> 0.80 ms at 35 %; 30 % 0.83, 40 % 0.91: profiles/r05/s32)
+#define RG_HOST_SPLIT_B_FIRST 1
 #endif
 rg_status render_host_split(const rg_scene *s, uint32_t W, uint32_t H, const rg_tiling *t, uint32_t rows,
                             uint8_t *rgba_out, rg_stats *stats) {
@@ -1272,7 +1277,8 @@ rg_status rg_render_host(const rg_scene *s, uint32_t W, uint32_t H, const rg_til
     // ms) -- banded there.
     if (!rgb_out) {
         const bool pinned = rg_host_device_ptr(rgba_out, std::max<size_t>((size_t)rows * W * 4, 1)) != nullptr;
-        if (s->image_bands == -2 && pinned && t->tile_stride == 1 && H >= 16)
+        const bool split = s->image_bands == -2 || (s->image_bands == 0 && !rg_heavy_path(rg_make_args(s)));
+        if (split && pinned && t->tile_stride == 1 && H >= 16)
             return render_host_split(s, W, H, t, rows, rgba_out, stats);
         bool direct = s->image_bands < 0;
         if (s->image_bands == 0) direct = pinned;
