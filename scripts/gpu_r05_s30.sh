@@ -16,3 +16,8 @@ for wl in synth1024; do
   timeout -k 10 300 python bench.py --workload $wl --gpus 2 --backend gloo --same-device --steps 6 --warmup 2 --no-extra --no-cpu-baseline > gpurun_out/s30/gloo_w2_$wl.json 2> gpurun_out/s30/gloo_w2_$wl.err
   tail -c 1500 gpurun_out/s30/gloo_w2_$wl.json; echo
 done
+echo "== compiler flag -amdgpu-use-amdgpu-trackers=1 (abvar/trk) vs HEAD"
+L="raingun_amd/libraingun_hip.so abvar/trk/libraingun_hip.so"
+bash scripts/ab_bench.sh "--workload test1 --no-extra --steps 200 --warmup 5" 3 $L
+bash scripts/ab_bench.sh "--workload synth1024 --no-extra --steps 200 --warmup 5" 3 $L
+bash scripts/ab_bench.sh "--workload synth4096p8d8 --width 1920 --height 1080 --no-extra --steps 60 --warmup 3" 2 $L
