@@ -2656,7 +2656,10 @@ extern "C" hipError_t rg_launch_tile_order(const RgKernelArgs *a, uint32_t *scra
 // One persistent block per CU slot: grid = CUs x (blocks per CU the register
 // and LDS budgets admit), capped by the tiles the frame has.
 #ifndef RG_LIGHT_PERSIST_BLOCKS_PER_CU
-#define RG_LIGHT_PERSIST_BLOCKS_PER_CU 8  // light persistent launches: one-wave blocks per CU (2 per SIMD)
+// light persistent launches: one-wave blocks per CU (8 -> 6 once they stopped prefetching tile slots:
+// test1 slowest 1/8 share 0.162-0.166 -> 0.153-0.156 ms, test3 0.139 -> 0.133; 4: 0.159, 12/16: slower;
+// profiles/r05/s34, s35)
+#define RG_LIGHT_PERSIST_BLOCKS_PER_CU 6
 #endif
 #ifndef RG_DEEP_BLOCKS_PER_CU
 #define RG_DEEP_BLOCKS_PER_CU 8  // deep-stack light launches: resident one-wave blocks per CU (bounds the frame buffer)
