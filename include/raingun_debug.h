@@ -29,6 +29,8 @@ typedef struct rg_bvh_info {
     float margin;          /* box inflation, scene units */
     float origin_bound;    /* rays with |o_k| above this scan all spheres */
     int32_t lane_stack;    /* per-lane walk: worst-case stack entries per lane */
+    int64_t lbuf_bytes;    /* shadow-ray light buffers + camera buffer, device bytes (capped:
+                            * RG_LB_TOTAL_WORDS words; lights past the cap keep the BVH walk) */
 } rg_bvh_info;
 rg_status rg_debug_set_bvh(rg_scene *scene, int32_t enable);
 rg_status rg_debug_bvh_info(const rg_scene *scene, rg_bvh_info *info);
@@ -37,8 +39,8 @@ rg_status rg_debug_bvh_info(const rg_scene *scene, rg_bvh_info *info);
  * a grid whose cells list every sphere a shadow ray starting there could hit,
  * so a shadow ray tests its cell's spheres instead of walking the BVH.  enable
  * 1 (default) / 0 (the BVH walk for every shadow ray); results are identical
- * either way.  rg_debug_lightbuf_count: lights with a buffer (0 when none was
- * built or the BVH is off). */
+ * either way.  rg_debug_lightbuf_count: lights whose buffer is in use (0 when
+ * none was built, the BVH is off, or the buffers are switched off). */
 rg_status rg_debug_set_lightbuf(rg_scene *scene, int32_t enable);
 int32_t rg_debug_lightbuf_count(const rg_scene *scene);
 
@@ -71,6 +73,12 @@ rg_status rg_debug_set_image_bands(rg_scene *scene, int32_t bands);
  * rendered into device memory and copied by DMA, the rest in one launch writing
  * host memory.  pct 1..99, 0 = the library default.  Results are identical. */
 rg_status rg_debug_set_host_split(rg_scene *scene, int32_t pct);
+
+/* Fault injection for the split path's error exits: the next `count` split renders
+ * report part A's launch as failed (RG_ERR_DEVICE) after part B -- the launch
+ * storing into the caller's buffer -- is already enqueued.  The call must still
+ * return only once nothing writes that buffer any more.  0 = off (default). */
+rg_status rg_debug_fail_split_a(rg_scene *scene, int32_t count);
 
 /* Tile shape of the one-launch host-visible path: log2 of the tile width,
  * 3 (8x8) .. 6 (64x1), every tile 64 pixels; wider tiles give whole row

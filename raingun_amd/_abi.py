@@ -111,7 +111,8 @@ class rg_tiling(C.Structure):
 
 class rg_bvh_info(C.Structure):  # include/raingun_debug.h
     _fields_ = [("built", C.c_int32), ("enabled", C.c_int32), ("nodes", C.c_int32), ("leaves", C.c_int32),
-                ("depth", C.c_int32), ("margin", C.c_float), ("origin_bound", C.c_float), ("lane_stack", C.c_int32)]
+                ("depth", C.c_int32), ("margin", C.c_float), ("origin_bound", C.c_float), ("lane_stack", C.c_int32),
+                ("lbuf_bytes", C.c_int64)]
 
 
 TILE_CALLBACK = C.CFUNCTYPE(C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8), C.c_void_p)
@@ -141,7 +142,7 @@ EXPORTED_SYMBOLS = (
 DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
                  "rg_debug_set_lightbuf", "rg_debug_lightbuf_count",
                  "rg_debug_set_tile_order", "rg_debug_set_lane_depth", "rg_debug_set_image_bands", "rg_debug_set_host_split",
-                 "rg_debug_set_host_tile_shape", "rg_debug_set_multi", "rg_debug_gather_noop")
+                 "rg_debug_fail_split_a", "rg_debug_set_host_tile_shape", "rg_debug_set_multi", "rg_debug_gather_noop")
 # include/raingun_frames.h
 FRAMES_SYMBOLS = ("rg_frames_create", "rg_frames_destroy", "rg_frames_step", "rg_frames_flush", "rg_frames_image",
                   "rg_frames_read_image", "rg_frames_status", "rg_frames_set_batch", "rg_comm_id_bytes",
@@ -207,8 +208,12 @@ def _declare(lib: C.CDLL) -> None:
     lib.rg_debug_set_lane_depth.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_set_image_bands.restype = C.c_int32
     lib.rg_debug_set_image_bands.argtypes = [C.c_void_p, C.c_int32]
-    lib.rg_debug_set_host_split.restype = C.c_int32
-    lib.rg_debug_set_host_split.argtypes = [C.c_void_p, C.c_int32]
+    if hasattr(lib, "rg_debug_set_host_split"):  # absent from pre-round-5 builds A/B runs load (RAINGUN_HIP_LIB)
+        lib.rg_debug_set_host_split.restype = C.c_int32
+        lib.rg_debug_set_host_split.argtypes = [C.c_void_p, C.c_int32]
+    if hasattr(lib, "rg_debug_fail_split_a"):  # absent from pre-round-6 builds
+        lib.rg_debug_fail_split_a.restype = C.c_int32
+        lib.rg_debug_fail_split_a.argtypes = [C.c_void_p, C.c_int32]
     if hasattr(lib, "rg_debug_set_multi"):  # absent from pre-round-3 builds
         lib.rg_debug_set_multi.restype = C.c_int32
         lib.rg_debug_set_multi.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32]

@@ -788,6 +788,8 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
             if (!rg_build_lightbuf(sp.data(), (int)h.sph.size(), h.lights[i].kind, h.lights[i].dn, h.lights[i].v,
                                    bvh.extent, (double)bvh.obound, lb))
                 continue;
+            // a budget on all buffers together: past it, a light keeps the BVH walk
+            if (h.lb_ent.size() + lb.ent.size() + h.lb_start.size() + lb.start.size() > RG_LB_TOTAL_WORDS) continue;
             const uint32_t ebase = (uint32_t)h.lb_ent.size(), cbase = (uint32_t)h.lb_start.size();
             for (uint32_t &v : lb.start) v += ebase;
             lb.dev.cell_off = cbase;
@@ -803,7 +805,8 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         const double zero[3] = {0.0, 0.0, 0.0};
         RgLightBufBuild cam;
         if (rg_build_lightbuf(sp.data(), (int)h.sph.size(), RG_LIGHT_SPHERICAL, zero, zero, bvh.extent,
-                              (double)bvh.obound, cam)) {
+                              (double)bvh.obound, cam) &&
+            h.lb_ent.size() + cam.ent.size() + h.lb_start.size() + cam.start.size() <= RG_LB_TOTAL_WORDS) {
             const uint32_t ebase = (uint32_t)h.lb_ent.size(), cbase = (uint32_t)h.lb_start.size();
             for (uint32_t &v : cam.start) v += ebase;
             cam.dev.cell_off = cbase;
@@ -817,6 +820,8 @@ rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out
         if (!built && s->lb_cam < 0) h.lbuf.clear();
         s->n_lbuf = built ? (int32_t)nl : 0;
         s->n_lbdesc = (int32_t)h.lbuf.size();
+        s->bvh_info.lbuf_bytes = (int64_t)((h.lb_ent.size() + h.lb_start.size()) * sizeof(uint32_t) +
+                                           h.lbuf.size() * sizeof(RgLightBufDev));
     }
     h.tex_w.resize(d->n_textures);
     h.tex_h.resize(d->n_textures);
@@ -1210,8 +1215,22 @@ rg_status render_host_split(const rg_scene *s, uint32_t W, uint32_t H, const rg_
     const bool light = !rg_heavy_path(rg_make_args(s));
     const uint32_t wl = (uint32_t)(s->host_tile_forced || !light ? s->host_tile_wlog : RG_HOST_TILE_WLOG_LIGHT);
     if (!ok(hipEventRecord(r.ev_t0, r.rs[0])) || !ok(hipStreamWaitEvent(r.rs[1], r.ev_t0, 0))) return RG_ERR_DEVICE;
+    // Once either part is enqueued, every exit first drains both render streams and the copy
+    // stream: part B's kernel and part A's DMA store into the caller's buffer, which the caller
+    // owns again when this call returns (rendering.rs:24-38 returns a finished ImageBuffer).
+    auto drain = [&](rg_status e) -> rg_status {
+        (void)hipStreamSynchronize(r.rs[1]);
+        (void)hipStreamSynchronize(r.rs[0]);
+        (void)hipStreamSynchronize(r.cs);
+        (void)hipGetLastError();
+        return e;
+    };
     // part A (device memory) and part B (one launch writing host memory), in RG_HOST_SPLIT_B_FIRST order
     auto launch_a = [&]() -> rg_status {
+        if (s->split_fail_a > 0) {  // rg_debug_fail_split_a: this launch reports failure without running
+            --s->split_fail_a;
+            return RG_ERR_DEVICE;
+        }
         const rg_status e = rg_launch_tiles(s, W, H, &t8, static_cast<uint8_t *>(r.d_rgba), nullptr, r.rs[0], r.h_snap,
                                             nullptr, false, nullptr, 0, nullptr, 3, false, false, 0, ja);
         if (e != RG_OK) return e;
@@ -1222,16 +1241,18 @@ rg_status render_host_split(const rg_scene *s, uint32_t W, uint32_t H, const rg_
                                false, nullptr, 0, nullptr, wl, true, false, ja, 0xFFFFFFFFu, true);  // image rows >= ja * 8
     };
     if (RG_HOST_SPLIT_B_FIRST) {
-        if ((st = launch_b()) != RG_OK || (st = launch_a()) != RG_OK) return st;
+        if ((st = launch_b()) != RG_OK || (st = launch_a()) != RG_OK) return drain(st);
     } else {
-        if ((st = launch_a()) != RG_OK || (st = launch_b()) != RG_OK) return st;
+        if ((st = launch_a()) != RG_OK || (st = launch_b()) != RG_OK) return drain(st);
     }
     if (!ok(hipStreamWaitEvent(r.cs, r.ev_done[0], 0)) ||
         !ok(hipMemcpyAsync(rgba_out, r.d_rgba, a_bytes, hipMemcpyDeviceToHost, r.cs)) ||
         !ok(hipEventRecord(r.ev_copy[0], r.cs)) || !ok(hipStreamWaitEvent(r.rs[1], r.ev_copy[0], 0)) ||
         !ok(hipEventRecord(r.ev_t1, r.rs[1])))
-        return RG_ERR_DEVICE;
-    if (!ok(hipStreamSynchronize(r.rs[1])) || !ok(hipStreamSynchronize(r.rs[0]))) return RG_ERR_DEVICE;
+        return drain(RG_ERR_DEVICE);
+    const bool synced1 = ok(hipStreamSynchronize(r.rs[1]));
+    const bool synced0 = ok(hipStreamSynchronize(r.rs[0]));
+    if (!synced1 || !synced0) return drain(RG_ERR_DEVICE);
     rg_stats total;
     std::memset(&total, 0, sizeof total);
     total.error_pixel = -1;
@@ -1519,7 +1540,8 @@ rg_status rg_debug_set_lightbuf(rg_scene *s, int32_t enable) {
 }
 
 int32_t rg_debug_lightbuf_count(const rg_scene *s) {
-    if (!s || !s->host || !s->bvh_enabled || s->n_nodes == 0) return 0;
+    // buffers IN USE: none while the BVH or the buffers are switched off (rg_debug_set_lightbuf(0))
+    if (!s || !s->host || !s->bvh_enabled || !s->lbuf_enabled || s->n_nodes == 0) return 0;
     int32_t n = 0;
     for (int32_t i = 0; i < s->n_lbuf; ++i) n += s->host->lbuf[(size_t)i].kind != RG_LB_NONE;
     return n;
@@ -1553,6 +1575,12 @@ rg_status rg_debug_set_image_bands(rg_scene *s, int32_t bands) {
 rg_status rg_debug_set_host_split(rg_scene *s, int32_t pct) {
     if (!s || pct < 0 || pct > 99) return RG_ERR_INVALID_ARGUMENT;
     s->host_split_pct = pct;
+    return RG_OK;
+}
+
+rg_status rg_debug_fail_split_a(rg_scene *s, int32_t count) {
+    if (!s || count < 0) return RG_ERR_INVALID_ARGUMENT;
+    s->split_fail_a = count;
     return RG_OK;
 }
 

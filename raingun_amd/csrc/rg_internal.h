@@ -180,6 +180,7 @@ struct rg_scene {
     int tile_order = -1;  // expensive tiles first (rg_kernels.hip "tile ordering"): -1 auto (heavy path), 0, 1
     int image_bands = 0;  // host-visible frames: 0 auto, -1 one launch writing host memory, -2 split, 1..16 row bands
     int host_split_pct = 0;  // -2 (split): percent of the frame's rows rendered into device memory + DMA (0: default)
+    mutable int split_fail_a = 0;  // debug: the next N split renders report part A's launch as failed (rg_debug_fail_split_a)
     int host_tile_wlog = RG_HOST_TILE_WLOG;  // tile shape of the one-launch host-visible path
     bool host_tile_forced = false;           // set by rg_debug_set_host_tile_shape (else light scenes: 64x1)
     // rg_render_multi (rg_debug_set_multi): 0 each device copies its rows to the host, 1 RCCL gather;

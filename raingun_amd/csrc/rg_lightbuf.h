@@ -36,6 +36,9 @@ bool rg_build_lightbuf(const double *spheres, int n, int kind, const double dn[3
 #ifndef RG_LB_MAX_ENTRIES
 #define RG_LB_MAX_ENTRIES (1u << 24)
 #endif
+#ifndef RG_LB_TOTAL_WORDS
+#define RG_LB_TOTAL_WORDS (1u << 25)  // every buffer of a scene together (entries + cell starts): 128 MiB
+#endif
 #ifndef RG_LB_CUBE_G
 #define RG_LB_CUBE_G 128  // spherical lights: cells per cube-face edge
 #endif

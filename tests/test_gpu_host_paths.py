@@ -153,6 +153,42 @@ def test_render_image_direct_many_frames(oracle_lib, example_scenes, kind, w, h,
         ds.close()
 
 
+def test_split_frame_error_exit_leaves_no_writer(example_scenes):
+    """the split host path (part B, a kernel storing into the caller's page-locked
+    frame, enqueued first) must not return while anything still writes that frame.  Part A's launch
+    is made to fail once (rg_debug_fail_split_a): the call returns RG_ERR_DEVICE, and at that moment
+    every row is either untouched (part A's, sentinel) or already final (part B's); nothing changes
+    afterwards; the next call renders the whole frame again."""
+    import copy
+    import time
+
+    s = copy.copy(example_scenes["test1"])
+    s.max_recursion_depth = 5
+    w, h = 3840, 2160
+    ds = DeviceScene(s)
+    ds.set_image_bands(-2)
+    ref = ds.render_image(w, h)
+    out = np.empty((h, w, 4), dtype=np.uint8)
+    reg = _abi.HostRegistration(out)
+    try:
+        out.fill(0xAB)
+        _abi.check(_abi.lib().rg_debug_fail_split_a(ds.handle, 1))
+        st = _abi.lib().rg_render_image(ds.handle, w, h, out.ctypes.data, None)
+        snap = out.copy()
+        assert st == _abi.RG_ERR_DEVICE
+        untouched = (snap == 0xAB).all(axis=(1, 2))
+        final = (snap == ref).all(axis=(1, 2))
+        assert (untouched | final).all(), np.flatnonzero(~(untouched | final))[:8]
+        assert final[-1] and untouched[0] and final.sum() > h // 2  # part B (the bottom ~65 %) ran to the end
+        time.sleep(0.2)
+        assert np.array_equal(out, snap)  # no kernel or DMA wrote the buffer after the call returned
+        ds.render_image(w, h, out=out)  # the injected failure does not stick
+        assert np.array_equal(out, ref)
+    finally:
+        reg.close()
+        ds.close()
+
+
 def test_render_image_4k_default_bands(oracle_lib, example_scenes):
     """BASELINE configs[1] through the drop-in itself: test1 3840x2160 depth 5,
     host-visible, the library's default band count."""

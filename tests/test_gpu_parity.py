@@ -130,6 +130,11 @@ def test_lightbuf_is_built_for_sphere_scenes():
     assert ds.lightbuf_count() == 3  # 1 directional + 2 spherical lights
     ds.set_bvh(False)
     assert ds.lightbuf_count() == 0  # the buffers ride on the BVH's bounds and path
+    ds.set_bvh(True)
+    ds.set_lightbuf(False)
+    assert ds.lightbuf_count() == 0  # built, but not in use
+    ds.set_lightbuf(True)
+    assert ds.lightbuf_count() == 3
     ds.close()
     ds = DeviceScene(_lights_scene())
     assert ds.lightbuf_count() >= 6
@@ -145,11 +150,36 @@ def test_lightbuf_stress_lights(oracle_lib, lightbuf, lane):
     _compare(oracle_lib, _lights_scene(), 192, 108, path=_abi.PATH_HEAVY, bvh=True, lane=lane, lightbuf=lightbuf)
 
 
+def _lights_scene_past_buffers():
+    """Eleven lights: more than the RG_LB_MAX_LIGHTS (8) that get a light buffer, so shadow rays of
+    lights 8.. walk the BVH, beside the camera buffer's slot in the same descriptor array."""
+    from raingun_amd.scene import DirectionalLight, SphericalLight
+
+    s = _lights_scene()
+    s.lights += [SphericalLight(position=(-20.0, 30.0, -60.0), color=Color(0.7, 1.0, 0.7), intensity=30000.0),
+                 DirectionalLight(direction=(0.5, -0.7, -0.2), color=Color(1.0, 1.0, 0.6), intensity=1.5),
+                 SphericalLight(position=(10.0, 2.0, -25.0), color=Color(0.9, 0.6, 1.0), intensity=5000.0)]
+    assert len(s.lights) == 11
+    return s
+
+
+@pytest.mark.parametrize("lightbuf", [True, False])
+def test_lightbuf_more_lights_than_buffers(oracle_lib, lightbuf):
+    """Lights beyond the buffered ones fall back to the BVH walk: both settings against
+    the CPU restatement on the 1024-sphere scene."""
+    s = _lights_scene_past_buffers()
+    ds = DeviceScene(s)
+    assert ds.lightbuf_count() <= 8
+    ds.close()
+    _compare(oracle_lib, s, 160, 90, path=_abi.PATH_HEAVY, bvh=True, lightbuf=lightbuf)
+
+
 def test_bvh_is_built_for_sphere_scenes():
     ds = DeviceScene(synthetic_scene(1024, 2, 5))
     info = ds.bvh_info()
     assert info.built == 1 and info.enabled == 1 and info.nodes > 64 and info.leaves >= 1024 // 4
     assert 0 < info.margin < 0.05 and info.origin_bound > 100
+    assert 0 < info.lbuf_bytes < 4 * (1 << 25)  # 3 lights + the camera buffer, under the scene's cap
     ds.set_bvh(False)
     assert ds.bvh_info().enabled == 0
     ds.close()
