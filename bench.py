@@ -550,7 +550,7 @@ def host_visible(workload: str, args, dev, W: int = 3840, H: int = 2160, budget_
                 reg.close()
         res[kind] = {"value": round(rays / dt / 1e6, 3), "ms_per_step": round(dt * 1e3, 4), "frames": n,
                      "frame_bytes": H * W * 4, "host_GBps": round(H * W * 4 / dt / 1e9, 2)}
-    res["multi_8gpu_rehearsal"] = multi_rehearsal(ds, W, H, res["pinned"]["ms_per_step"], args)
+    res["multi_8gpu_rehearsal"] = multi_rehearsal(ds, W, H, res["pinned"]["ms_per_step"], args, split=True)
     ds.close()
     torch.cuda.synchronize(dev)
     res["value"] = res["pinned"]["value"]
@@ -559,20 +559,26 @@ def host_visible(workload: str, args, dev, W: int = 3840, H: int = 2160, budget_
     return res
 
 
-def multi_rehearsal(ds, W: int, H: int, one_gpu_ms: float, args, n: int = 8, budget_s: float = 0.5):
+def multi_rehearsal(ds, W: int, H: int, one_gpu_ms: float, args, n: int = 8, budget_s: float = 0.5,
+                    split: bool = False):
     """rg_render_multi's host-visible frame on an n-GPU node, rehearsed on one GPU: each device's
-    timeline -- its row tiles rendered in bands, each band's rows copied over ITS OWN PCIe link
-    straight into the caller's page-locked buffer (rg_multi.hip, direct mode) -- timed alone
-    (rg_debug_set_multi stand-in, only_rank = r) for every r.  The frame is done when the slowest
-    device is: projected frame time = max over r.  A projection (this GPU's link stands for each
-    device's own; host memory bandwidth assumed to take n links at once), not a measurement."""
+    timeline -- its 8-row tiles rendered as ONE launch whose kernel stores the finished rows over
+    ITS OWN PCIe link straight into the caller's page-locked buffer (rg_multi.hip render_direct_one;
+    light scenes since round 6, trace-heavy scenes since round 4) -- timed alone (rg_debug_set_multi
+    stand-in, only_rank = r) for every r.  The frame is done when the slowest device is: projected
+    frame time = max over r.  A projection (this GPU's link stands for each device's own; host
+    memory bandwidth assumed to take n links at once), not a measurement.  split: also time, per
+    device, its share rendered device-resident (one launch, HIP events: `render_ms`) and one D2H copy
+    of that many rows into pinned memory (`copy_ms`); overlap = render + copy - timeline."""
     import numpy as np
+    import torch
 
     from raingun_amd import _abi
 
     buf = np.empty((H, W, 4), dtype=np.uint8)
     reg = _abi.HostRegistration(buf)
-    per_rank = []
+    per_rank, render, copy = [], [], []
+    lib = _abi.lib()
     try:
         for r in range(n):
             ds.set_multi(0, stand_in=True, bands=0, only_rank=r)
@@ -583,14 +589,44 @@ def multi_rehearsal(ds, W: int, H: int, one_gpu_ms: float, args, n: int = 8, bud
                 ds.render_multi(W, H, n, 8, out=buf)
                 k += 1
             per_rank.append((time.perf_counter() - t0) / k * 1e3)
+            if split:
+                t = _abi.rg_tiling(8, n, r)
+                rows = lib.rg_tiling_rows(H, C.byref(t))
+                part = torch.empty((rows, W, 4), dtype=torch.uint8, device="cuda")
+                host = torch.empty((rows, W, 4), dtype=torch.uint8, pin_memory=True)
+                st = _abi.rg_stats()
+                ks = []
+                for i in range(7):
+                    _abi.check(lib.rg_render_tiles_async(ds.handle, W, H, C.byref(t), C.c_void_p(part.data_ptr()),
+                                                         None, None, C.byref(st)))
+                    if i >= 2:
+                        ks.append(st.kernel_ms)
+                render.append(float(np.median(ks)))
+                cs = []
+                for i in range(7):
+                    torch.cuda.synchronize()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    host.copy_(part, non_blocking=True)
+                    e1.record()
+                    e1.synchronize()
+                    if i >= 2:
+                        cs.append(e0.elapsed_time(e1))
+                copy.append(float(np.median(cs)))
     finally:
         ds.set_multi(0, stand_in=False, bands=0, only_rank=-1)
         reg.close()
     proj = max(per_rank)
-    return {"projected_ms_per_step": round(proj, 4), "projected_speedup_vs_1gpu": round(one_gpu_ms / proj, 2),
-            "per_device_ms": [round(x, 4) for x in per_rank], "n_gpus": n,
-            "basis": "one GPU times each device's rg_render_multi timeline alone (banded render of its 8-row tiles + "
-                     "its rows' strided copies into the pinned caller buffer); projected frame = the slowest device"}
+    out = {"projected_ms_per_step": round(proj, 4), "projected_speedup_vs_1gpu": round(one_gpu_ms / proj, 2),
+           "per_device_ms": [round(x, 4) for x in per_rank], "n_gpus": n,
+           "basis": "one GPU times each device's rg_render_multi timeline alone (its 8-row tiles as one launch "
+                    "storing its rows into the pinned caller buffer over its own link); projected frame = the "
+                    "slowest device"}
+    if split:
+        out["per_device_split"] = [{"timeline_ms": round(tl, 4), "render_ms": round(rm, 4), "copy_ms": round(cm, 4),
+                                    "overlap_ms": round(rm + cm - tl, 4)}
+                                   for tl, rm, cm in zip(per_rank, render, copy)]
+    return out
 
 
 # Extra line items: (key, workload, size, CPU baseline?) -- BASELINE configs[2..4] and the north_star scene.

@@ -80,6 +80,15 @@ rg_status rg_debug_set_host_split(rg_scene *scene, int32_t pct);
  * return only once nothing writes that buffer any more.  0 = off (default). */
 rg_status rg_debug_fail_split_a(rg_scene *scene, int32_t count);
 
+/* Light-path frames into page-locked host memory (the one-launch host-frame kernels; -1 keeps a
+ * setting): finished tiles per LDS-ring flush (1..16, 0 = 16) and consecutive tiles the tile
+ * queue hands a wave at a time (0 = the flush size), for launches below 50,000 tiles (`_small`:
+ * rg_render_multi's device shares) and from it (`_big`: whole frames);
+ * `multi_light_one` 1 (default) = rg_render_multi's automatic mode renders a light scene's device
+ * shares as one launch each, 0 = bands + DMA copies.  Results are identical for every setting. */
+rg_status rg_debug_set_host_ring(rg_scene *scene, int32_t flush_small, int32_t group_small, int32_t flush_big,
+                                 int32_t group_big, int32_t multi_light_one);
+
 /* Tile shape of the one-launch host-visible path: log2 of the tile width,
  * 3 (8x8) .. 6 (64x1), every tile 64 pixels; wider tiles give whole row
  * segments per PCIe write.  0 = automatic (the default: 16x4 for heavy-path
@@ -111,6 +120,10 @@ int rg_debug_gather_noop(const void *send, void *recv, size_t count, int datatyp
  * counts, [4..8] BVH traversal statistics when the library was built with
  * -DRG_BVH_STATS (zero otherwise). */
 rg_status rg_debug_counters(const rg_scene *scene, uint64_t out[16]);
+
+/* Words [first, first + n) of the last render's counter set (RG_COUNTER_WORDS words):
+ * diagnostic builds' extra statistics, e.g. -DRG_REGION_STATS region visits at 144.. */
+rg_status rg_debug_counter_words(const rg_scene *scene, int32_t first, int32_t n, uint64_t *out);
 
 #ifdef __cplusplus
 }

@@ -142,7 +142,8 @@ EXPORTED_SYMBOLS = (
 DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "rg_debug_counters",
                  "rg_debug_set_lightbuf", "rg_debug_lightbuf_count",
                  "rg_debug_set_tile_order", "rg_debug_set_lane_depth", "rg_debug_set_image_bands", "rg_debug_set_host_split",
-                 "rg_debug_fail_split_a", "rg_debug_set_host_tile_shape", "rg_debug_set_multi", "rg_debug_gather_noop")
+                 "rg_debug_fail_split_a", "rg_debug_set_host_ring", "rg_debug_set_host_tile_shape", "rg_debug_set_multi", "rg_debug_gather_noop",
+                 "rg_debug_counter_words")
 # include/raingun_frames.h
 FRAMES_SYMBOLS = ("rg_frames_create", "rg_frames_destroy", "rg_frames_step", "rg_frames_flush", "rg_frames_image",
                   "rg_frames_read_image", "rg_frames_status", "rg_frames_set_batch", "rg_comm_id_bytes",
@@ -211,6 +212,9 @@ def _declare(lib: C.CDLL) -> None:
     if hasattr(lib, "rg_debug_set_host_split"):  # absent from pre-round-5 builds A/B runs load (RAINGUN_HIP_LIB)
         lib.rg_debug_set_host_split.restype = C.c_int32
         lib.rg_debug_set_host_split.argtypes = [C.c_void_p, C.c_int32]
+    if hasattr(lib, "rg_debug_set_host_ring"):  # absent from pre-round-6 builds
+        lib.rg_debug_set_host_ring.restype = C.c_int32
+        lib.rg_debug_set_host_ring.argtypes = [C.c_void_p] + [C.c_int32] * 5
     if hasattr(lib, "rg_debug_fail_split_a"):  # absent from pre-round-6 builds
         lib.rg_debug_fail_split_a.restype = C.c_int32
         lib.rg_debug_fail_split_a.argtypes = [C.c_void_p, C.c_int32]
@@ -222,6 +226,9 @@ def _declare(lib: C.CDLL) -> None:
         lib.rg_debug_set_host_tile_shape.argtypes = [C.c_void_p, C.c_int32]
     lib.rg_debug_counters.restype = C.c_int32
     lib.rg_debug_counters.argtypes = [C.c_void_p, P(C.c_uint64)]
+    if hasattr(lib, "rg_debug_counter_words"):  # absent from pre-round-6 builds
+        lib.rg_debug_counter_words.restype = C.c_int32
+        lib.rg_debug_counter_words.argtypes = [C.c_void_p, C.c_int32, C.c_int32, P(C.c_uint64)]
     lib.rg_frames_create.restype = C.c_int32
     lib.rg_frames_create.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_int32,
                                      C.c_int32, C.c_void_p, C.c_void_p, P(C.c_void_p)]
@@ -271,7 +278,7 @@ def lib() -> C.CDLL:
     """Load libraingun_hip.so (built by ``make -C raingun_amd/csrc``).  Raises if absent."""
     global _LIB
     if _LIB is None:
-        path = os.environ.get("RAINGUN_HIP_LIB", str(LIB_PATH))
+        path = os.environ.get("RAINGUN_HIP_LIB") or str(LIB_PATH)
         if not Path(path).exists():
             raise RuntimeError(
                 f"{path} is missing: build it with `make -C raingun_amd/csrc` (or __graft_entry__.build()). "

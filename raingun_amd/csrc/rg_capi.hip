@@ -320,6 +320,11 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     // host-frame features (rg_kernels.hip HF) up to rg_host_array_frames() frames;
     // the others the MAXD == 0 kernels, whose frames live in a global buffer
     const bool host_arrays = frames <= rg_host_array_frames() && rg_heavy_path(a);
+    if (host_frame) {  // the light path's LDS tile ring (rg_device.h RG_RING_*)
+        const bool big = rg_tile_count(a) >= RG_RING_BIG_TILES;
+        a.ring_flush = (uint32_t)std::max(0, big ? s->ring_flush_big : s->ring_flush_small);
+        a.ring_group = (uint32_t)std::max(0, big ? s->ring_group_big : s->ring_group_small);
+    }
     const int disp = (host_frame && !host_arrays) ? std::max(frames, rg_max_array_frames() + 1) : frames;
     if (rg_launch_global_frames(&a, disp) && out_rows > 0) {
         // frames in a global buffer sized for this launch's (persistent) grid
@@ -601,6 +606,10 @@ void rg_sync_settings(rg_scene *dst, const rg_scene *src) {
     dst->lbuf_enabled = src->lbuf_enabled;
     dst->lane_min_depth = src->lane_min_depth;
     dst->tile_order = src->tile_order;
+    dst->ring_flush_small = src->ring_flush_small;
+    dst->ring_group_small = src->ring_group_small;
+    dst->ring_flush_big = src->ring_flush_big;
+    dst->ring_group_big = src->ring_group_big;
 }
 
 extern "C" {
@@ -1578,6 +1587,19 @@ rg_status rg_debug_set_host_split(rg_scene *s, int32_t pct) {
     return RG_OK;
 }
 
+rg_status rg_debug_set_host_ring(rg_scene *s, int32_t flush_small, int32_t group_small, int32_t flush_big,
+                                  int32_t group_big, int32_t multi_light_one) {
+    if (!s || flush_small < -1 || flush_small > 16 || group_small < -1 || flush_big < -1 || flush_big > 16 ||
+        group_big < -1 || multi_light_one < -1 || multi_light_one > 1)
+        return RG_ERR_INVALID_ARGUMENT;
+    if (flush_small >= 0) s->ring_flush_small = flush_small;
+    if (group_small >= 0) s->ring_group_small = group_small;
+    if (flush_big >= 0) s->ring_flush_big = flush_big;
+    if (group_big >= 0) s->ring_group_big = group_big;
+    if (multi_light_one >= 0) s->multi_light_one = multi_light_one != 0;
+    return RG_OK;
+}
+
 rg_status rg_debug_fail_split_a(rg_scene *s, int32_t count) {
     if (!s || count < 0) return RG_ERR_INVALID_ARGUMENT;
     s->split_fail_a = count;
@@ -1596,6 +1618,15 @@ rg_status rg_debug_counters(const rg_scene *s, uint64_t out[16]) {
     if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
     if (!ok(hipStreamSynchronize(s->last->stream)) ||
         !ok(hipMemcpy(out, s->last->last_counters, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost)))
+        return RG_ERR_DEVICE;
+    return RG_OK;
+}
+
+rg_status rg_debug_counter_words(const rg_scene *s, int32_t first, int32_t n, uint64_t *out) {
+    if (!s || !out || first < 0 || n < 0 || first + n > RG_COUNTER_WORDS) return RG_ERR_INVALID_ARGUMENT;
+    if (!ok(hipSetDevice(s->device))) return RG_ERR_DEVICE;
+    if (!ok(hipStreamSynchronize(s->last->stream)) ||
+        !ok(hipMemcpy(out, s->last->last_counters + first, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost)))
         return RG_ERR_DEVICE;
     return RG_OK;
 }

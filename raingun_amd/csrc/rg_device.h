@@ -198,6 +198,11 @@ struct RgKernelArgs {
     int32_t n_lbuf;
     int32_t lb_cam;            // >= 0: lbuf[lb_cam] is the camera buffer (a light buffer at the origin, primary rays)
     uint32_t lds_lbuf;         // LDS arena: the light-buffer descriptors (hot tables, after the texture descriptors)
+    // light path into page-locked host memory (defer_px, LDS tile ring): finished tiles per ring flush
+    // (1 .. RG_HOST_RING) and consecutive tiles the queue hands a wave at a time (1 .. ring_flush);
+    // 0 = RG_HOST_RING for both.  Small launches (rg_render_multi's shares) want small groups (balance),
+    // whole frames long runs of host memory per flush (rg_capi.hip host_ring_for)
+    uint32_t ring_flush, ring_group;
 };
 
 __host__ __device__ inline uint32_t rg_tile_w(const RgKernelArgs &a) { return 1u << a.tile_wlog; }
@@ -211,6 +216,30 @@ __host__ __device__ inline unsigned long long rg_tile_count(const RgKernelArgs &
 // sizeof(Frame) in rg_kernels.hip (the deep frame buffer is sized on the host)
 #define RG_FRAME_BYTES 88
 
+// Light-path frames into page-locked host memory (the one-launch host-frame kernels' LDS tile ring,
+// rg_kernels.hip): finished tiles per ring flush and consecutive tiles per queue slot, for launches
+// below RG_RING_BIG_TILES 64-pixel tiles (rg_render_multi's device shares: balance over the waves)
+// and from it (whole frames, part B of split frames: long runs of host memory per flush).  test1 4K
+// (profiles/r06/s5/hv_ring_sweep.out): 8-device rehearsal 0.2895 ms banded -> 0.207 ms one launch
+// at 4 / 1 (16 / 16: 0.241, 4 / 4: 0.273); the 1-GPU pinned frame 0.805 -> 0.768 ms at 8 / 8.
+#ifndef RG_RING_FLUSH_SMALL
+#define RG_RING_FLUSH_SMALL 4
+#endif
+#ifndef RG_RING_GROUP_SMALL
+#define RG_RING_GROUP_SMALL 1
+#endif
+#ifndef RG_RING_FLUSH_BIG
+#define RG_RING_FLUSH_BIG 8
+#endif
+#ifndef RG_RING_GROUP_BIG
+#define RG_RING_GROUP_BIG 8
+#endif
+#ifndef RG_RING_BIG_TILES
+#define RG_RING_BIG_TILES 50000u
+#endif
+#ifndef RG_MULTI_LIGHT_ONE
+#define RG_MULTI_LIGHT_ONE 1  // rg_render_multi, automatic mode: light scenes' shares as one launch per device
+#endif
 #ifndef RG_LB
 #define RG_LB 3                   // lights per shadow batch on the light path (its LB template parameter)
 #endif

@@ -180,7 +180,13 @@ struct rg_scene {
     int tile_order = -1;  // expensive tiles first (rg_kernels.hip "tile ordering"): -1 auto (heavy path), 0, 1
     int image_bands = 0;  // host-visible frames: 0 auto, -1 one launch writing host memory, -2 split, 1..16 row bands
     int host_split_pct = 0;  // -2 (split): percent of the frame's rows rendered into device memory + DMA (0: default)
-    mutable int split_fail_a = 0;  // debug: the next N split renders report part A's launch as failed (rg_debug_fail_split_a)
+    mutable int split_fail_a = 0;
+    // light-path host frames (rg_debug_set_host_ring): LDS-ring flush size and queue group of small
+    // (< RG_RING_BIG_TILES tiles) and big launches; rg_render_multi's automatic mode runs light
+    // scenes' shares as one launch per device (else bands + DMA)
+    int ring_flush_small = RG_RING_FLUSH_SMALL, ring_group_small = RG_RING_GROUP_SMALL;
+    int ring_flush_big = RG_RING_FLUSH_BIG, ring_group_big = RG_RING_GROUP_BIG;
+    bool multi_light_one = RG_MULTI_LIGHT_ONE != 0;  // debug: the next N split renders report part A's launch as failed (rg_debug_fail_split_a)
     int host_tile_wlog = RG_HOST_TILE_WLOG;  // tile shape of the one-launch host-visible path
     bool host_tile_forced = false;           // set by rg_debug_set_host_tile_shape (else light scenes: 64x1)
     // rg_render_multi (rg_debug_set_multi): 0 each device copies its rows to the host, 1 RCCL gather;

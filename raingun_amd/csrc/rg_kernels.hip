@@ -147,6 +147,30 @@ __device__ __forceinline__ bool disk_hit(const RgDsk &k, V3 o, V3 d, double &t) 
     return true;
 }
 
+// Region visit counts (diagnostic build -DRG_REGION_STATS; scripts/region_stats.py): every time a
+// wave enters region k, its first active lane adds 1 to counters[RG_REGION_BASE + 2k] and the
+// active lanes to [+ 2k + 1] -- the dynamic weights of the static ISA budget (scripts/isa_budget.py).
+// Words 144.. lie in the lines of tile-queue heads 8-15, unused with RG_NQ = 8.
+#define RG_REGION_BASE 144
+enum : int {
+    RGR_LOOP = 0, RGR_PRIM, RGR_PRIM_SPH_TAIL, RGR_PRIM_PLANE_DIV, RGR_GETCOLOR, RGR_NORMAL_SPHERE,
+    RGR_BATCH, RGR_TEXEL, RGR_UV_SPHERE, RGR_UV_PLANE, RGR_LIGHT_SPH, RGR_REFRACT, RGR_SHADE, RGR_UNWIND,
+    RGR_UNWIND_STEP, RGR_TILE_FETCH, RGR_Q_CLOSEST, RGR_Q_SHADOW, RGR_SH_GROUP, RGR_SH_TAIL, RGR_SH_PLANE,
+    RGR_SH_PLANE_DIV, RGR_QC_GROUP, RGR_QC_TAIL, RGR_QC_PLANE, RGR_PRIM_GROUP, RGR_PRIM_PLANE, RGR_DISK, RGR_BOX, RGR_COUNT
+};
+#ifdef RG_REGION_STATS
+#define RG_REGION(k)                                                                                  \
+    do {                                                                                              \
+        const unsigned long long m_ = __ballot(1);                                                    \
+        if ((int)(threadIdx.x & 63u) == __builtin_ffsll((long long)m_) - 1) {                         \
+            atomicAdd(&a.counters[RG_REGION_BASE + 2 * (k)], 1ull);                                   \
+            atomicAdd(&a.counters[RG_REGION_BASE + 2 * (k) + 1], (unsigned long long)__builtin_popcountll(m_)); \
+        }                                                                                             \
+    } while (0)
+#else
+#define RG_REGION(k) do { } while (0)
+#endif
+
 // ---------------------------------------------------------------- sphere sources
 // The sphere tables are read with a wave-uniform index.  Three sources:
 //  * SphLds: the persistent block stages the tables into LDS once and every
@@ -266,6 +290,7 @@ __device__ __forceinline__ void sph_primary_group(const RgKernelArgs &a, const S
     double cc[G], adj[G], opp[G];
     bool cand[G];
     bool any = false;
+    RG_REGION(RGR_PRIM_GROUP);
 #pragma unroll
     for (int k = 0; k < G; ++k) { s[k] = src.get(i + k); cc[k] = src.getcc(i + k); }
 #pragma unroll
@@ -276,6 +301,7 @@ __device__ __forceinline__ void sph_primary_group(const RgKernelArgs &a, const S
         any |= cand[k];
     }
     if (any) {
+        RG_REGION(RGR_PRIM_SPH_TAIL);
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             double t;
@@ -335,6 +361,7 @@ __device__ __forceinline__ void sph_query_group(const RgKernelArgs &a, const Src
     double adj[G], opp[G];
     bool cand[G];
     bool any = false;
+    RG_REGION(RGR_QC_GROUP);
 #pragma unroll
     for (int k = 0; k < G; ++k) s[k] = src.get(i + k);
 #pragma unroll
@@ -346,6 +373,7 @@ __device__ __forceinline__ void sph_query_group(const RgKernelArgs &a, const Src
         any |= cand[k];
     }
     if (any && need) {
+        RG_REGION(RGR_QC_TAIL);
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             double t;
@@ -764,23 +792,28 @@ __device__ __forceinline__ void trace_primary(const RgKernelArgs &a, const Src &
         if (a.lb_cam >= 0) cam = lbuf_begin(a, src, a.lb_cam, d, 0.0, 0.0, 0.0);
     }
     for (int i = 0; i < a.n_pln; ++i) {
+        RG_REGION(RGR_PRIM_PLANE);
         const RgPln p = src.getp(i);
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137
         if (den > 1e-6) {
+            RG_REGION(RGR_PRIM_PLANE_DIV);
             double dist = p.on / den;                           // v = o_p - 0 = o_p: v.n = o.n
             if (dist >= 0.0) closest_add(c, dist, rg_cptr(a.pln_id)[i]);
         }
     }
     const V3 o = v3(0.0, 0.0, 0.0);
     for (int i = 0; i < a.n_dsk; ++i) {
+        RG_REGION(RGR_DISK);
         const RgDsk k = src.getd(i);
         double t;
         if (disk_hit(k, o, d, t)) closest_add(c, t, rg_cptr(a.dsk_id)[i]);
     }
     if (a.n_box > 0) {
+        RG_REGION(RGR_BOX);
         V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);           // ray.rs:24
         int sx = inv.x < 0.0, sy = inv.y < 0.0, sz = inv.z < 0.0;
         for (int i = 0; i < a.n_box; ++i) {
+            RG_REGION(RGR_BOX);
             const RgBox b = src.getb(i);
             double t;
             if (aabb_hit(b, o, inv, sx, sy, sz, t)) closest_add(c, t, rg_cptr(a.box_id)[i]);
@@ -828,6 +861,7 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
     for (int i = 0; i < a.n_pln; ++i) {
         const RgPln p = src.getp(i);
         double den = (p.nx * d.x + p.ny * d.y) + p.nz * d.z;   // bodies.rs:137-148
+        RG_REGION(RGR_QC_PLANE);
         if (den > 1e-6 && need) {
             double vx = p.ox - o.x, vy = p.oy - o.y, vz = p.oz - o.z;
             double dist = ((vx * p.nx + vy * p.ny) + vz * p.nz) / den;
@@ -842,6 +876,7 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
     }
     if (!__any(need)) return;
     for (int i = 0; i < a.n_dsk; ++i) {
+        RG_REGION(RGR_DISK);
         const RgDsk k = src.getd(i);
         double t;
         if (need && disk_hit(k, o, d, t)) {
@@ -853,9 +888,11 @@ __device__ __forceinline__ void trace_query(const RgKernelArgs &a, const Src &sr
         }
     }
     if (a.n_box > 0 && __any(need)) {
+        RG_REGION(RGR_BOX);
         V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
         int sx = inv.x < 0.0, sy = inv.y < 0.0, sz = inv.z < 0.0;
         for (int i = 0; i < a.n_box; ++i) {
+            RG_REGION(RGR_BOX);
             const RgBox b = src.getb(i);
             double t;
             if (need && aabb_hit(b, o, inv, sx, sy, sz, t)) {
@@ -944,6 +981,7 @@ __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &s
     const int n = a.n_sph, nfull = n - n % G;
     for (int i = 0; i < n;) {
         const int g = i < nfull ? G : 1;  // wave-uniform
+        RG_REGION(RGR_SH_GROUP);
         RgSph s[G];
         double hx[G], hy[G], hz[G], hh[G], adj[G][LB], opp[G][LB];
         bool cand[G][LB];
@@ -964,6 +1002,7 @@ __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &s
             }
         }
         if (any) {
+            RG_REGION(RGR_SH_TAIL);
 #pragma unroll
             for (int k = 0; k < G; ++k) {
 #pragma unroll
@@ -982,6 +1021,7 @@ __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &s
         const RgPln p = src.getp(i);
         const double vx = p.ox - o.x, vy = p.oy - o.y, vz = p.oz - o.z;     // bodies.rs:139
         const double num = (vx * p.nx + vy * p.ny) + vz * p.nz;             // :140 numerator
+        RG_REGION(RGR_SH_PLANE);
 #pragma unroll
         for (int l = 0; l < LB; ++l) {
             const double den = (p.nx * sb.d[l].x + p.ny * sb.d[l].y) + p.nz * sb.d[l].z;  // :137
@@ -990,6 +1030,7 @@ __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &s
                 if (sb.ld[l] == __builtin_inf() && num >= 0.0) {
                     hit = true;  // fl(num/den) >= 0 and !(fl(num/den) > inf): no division needed
                 } else {
+                    RG_REGION(RGR_SH_PLANE_DIV);
                     const double dist = num / den;
                     hit = dist >= 0.0 && !(dist > sb.ld[l]);
                 }
@@ -999,6 +1040,7 @@ __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &s
     }
     if (!__any(occl != full)) return;
     for (int i = 0; i < a.n_dsk; ++i) {
+        RG_REGION(RGR_DISK);
         const RgDsk k = src.getd(i);
 #pragma unroll
         for (int l = 0; l < LB; ++l) {
@@ -1007,12 +1049,14 @@ __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &s
         }
     }
     if (a.n_box > 0 && __any(occl != full)) {
+        RG_REGION(RGR_BOX);
 #pragma unroll
         for (int l = 0; l < LB; ++l) {
             const V3 d = sb.d[l];
             const V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
             const int sx = inv.x < 0.0, sy = inv.y < 0.0, sz = inv.z < 0.0;
             for (int i = 0; i < a.n_box; ++i) {
+                RG_REGION(RGR_BOX);
                 const RgBox b = src.getb(i);
                 double t;
                 if (!((occl >> l) & 1u) && aabb_hit(b, o, inv, sx, sy, sz, t) && !(t > sb.ld[l])) occl |= 1u << l;
@@ -1657,6 +1701,9 @@ void rg_render_kernel(RgKernelArgs a) {
     const C3 def = c3(a.def[0], a.def[1], a.def[2]);
     const int max_depth = (int)a.max_depth;
     [[maybe_unused]] const bool use_ring = RING > 0 && a.defer_px;
+    // the launch's ring flush size and queue group (RgKernelArgs::ring_flush / ring_group)
+    [[maybe_unused]] const uint32_t ring_n = RING > 0 ? (a.ring_flush ? min(a.ring_flush, (uint32_t)(RING > 0 ? RING : 1)) : (uint32_t)RING) : 1u;
+    [[maybe_unused]] const uint32_t ring_g = RING > 0 ? (a.ring_group ? min(a.ring_group, ring_n) : ring_n) : 1u;
     // store the ring's tiles: each lane its pixel of every tile (same index rule as the tile start)
     [[maybe_unused]] auto flush_ring = [&]() {
         for (uint32_t k = 0; k < nring; ++k) {
@@ -1722,6 +1769,7 @@ void rg_render_kernel(RgKernelArgs a) {
     uint32_t tile_iters = 0;
 #endif
     for (;;) {
+        RG_REGION(RGR_LOOP);
         if constexpr (LB == 1 && TASKS && RG_SHADOW_FAN > 0) {
             // shadow fan-out, collect: the helpers' occlusion bits (every lane active here)
             if (__any(nfan > 0)) {
@@ -1752,6 +1800,8 @@ void rg_render_kernel(RgKernelArgs a) {
                     // get_color (rendering.rs:80-120)
                     const RgBodyDev b = T.bodies[c.id];
                     const RgMatDev m = T.mats[c.id];
+                    RG_REGION(RGR_GETCOLOR);
+                    if (b.kind == RG_BODY_SPHERE) RG_REGION(RGR_NORMAL_SPHERE);
                     V3 h = add(q.o, scl(q.d, c.t));
                     V3 n;
                     if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
@@ -1765,6 +1815,14 @@ void rg_render_kernel(RgKernelArgs a) {
                             // 0.2955 ms over 200 frames, profiles/r04/s15/session.txt)
                             const bool textured = m.coloration != RG_COLORATION_COLOR;
                             uint32_t texel = 0u;
+                            RG_REGION(RGR_BATCH);
+#ifdef RG_REGION_STATS
+                            if (textured) {
+                                RG_REGION(RGR_TEXEL);
+                                if (b.kind == RG_BODY_SPHERE) RG_REGION(RGR_UV_SPHERE);
+                                else if (b.kind != RG_BODY_AABB) RG_REGION(RGR_UV_PLANE);
+                            }
+#endif
                             if (textured) texel = texel_fetch(T.texs, m, b, h);
                             else { park[64 * PK_COL] = m.color[0]; park[64 * (PK_COL + 1)] = m.color[1]; park[64 * (PK_COL + 2)] = m.color[2]; }
                             park[64 * PK_REFL] = m.albedo_pi;                       // rendering.rs:164
@@ -1785,6 +1843,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             for (int l = 0; l < LB; ++l) {
                                 if (l < a.n_lights) {
                                     const RgLightDev L = T.lights[l];
+                                    if (L.kind != RG_LIGHT_DIRECTIONAL) RG_REGION(RGR_LIGHT_SPH);
                                     light_dir_dist(L, h, sb.d[l], sb.ld[l]);
                                     park[64 * (PK_PP + l)] = fmaxf((float)dot(n, sb.d[l]), 0.0f);  // rendering.rs:161-162
                                     park[64 * (PK_LIN + l)] = light_intensity(L, h);               // pure; used if lit
@@ -1814,6 +1873,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             shade = true;
                         }
                     } else {
+                        RG_REGION(RGR_REFRACT);
                         float kr = (float)fresnel(q.d, n, m.index);
                         C3 surf = surface_color(T.texs, m, b, h);
                         int cd = qdepth + 1;
@@ -1882,6 +1942,7 @@ void rg_render_kernel(RgKernelArgs a) {
             }
             if constexpr (LB > 1) {
               if (shade) {
+                RG_REGION(RGR_SHADE);
                 // shade_diffuse accumulation over the batch (rendering.rs:141-170), in light order
                 const C3 bc = c3(park[64 * PK_COL], park[64 * (PK_COL + 1)], park[64 * (PK_COL + 2)]);
                 const float refl = park[64 * PK_REFL];
@@ -1990,7 +2051,9 @@ void rg_render_kernel(RgKernelArgs a) {
                 }
             }
             if (unwind) {
+                RG_REGION(RGR_UNWIND);
                 for (;;) {
+                    RG_REGION(RGR_UNWIND_STEP);
                     if (sp == 0) {
                         bool handed = false;
                         if constexpr (TASKS) {
@@ -2074,7 +2137,7 @@ void rg_render_kernel(RgKernelArgs a) {
                 if (use_ring) {
                     ring_px[rw][nring][lane] = *my_px;
                     if (lane == 0) ring_tile[rw][nring] = my_tile;
-                    if (++nring == (uint32_t)RING) flush_ring();
+                    if (++nring == ring_n) flush_ring();
                     ringed = true;
                 }
             }
@@ -2083,6 +2146,7 @@ void rg_render_kernel(RgKernelArgs a) {
         }
         // a wave with no live lane takes the next tile
         if (tiles_left && !__any(mode != MODE_DONE)) {
+            RG_REGION(RGR_TILE_FETCH);
 #ifdef RG_TILE_TIMES
             if (cur_tile != 0xFFFFFFFFu && lane == 0 && a.rgb) {
                 a.rgb[cur_tile] = (float)(wall_clock64() - t_tile) * 0.01f;  // 100 MHz clock
@@ -2103,7 +2167,7 @@ void rg_render_kernel(RgKernelArgs a) {
             }
             // ring mode: the queue hands out groups of RING consecutive tiles (one contiguous
             // run of host memory per ring flush: 4 KB with 64x1 tiles)
-            const uint32_t qlimit = (RING > 0 && use_ring) ? (ntiles + RING - 1) / RING : ntiles;
+            const uint32_t qlimit = (RING > 0 && use_ring) ? (ntiles + ring_g - 1) / ring_g : ntiles;
             // Tile-slot prefetch (light path, device-resident launches): the slot claimed at the
             // previous tile's start, so the atomic's round trip overlaps that tile (round 4, same
             // box, interleaved: test1 0.2972 -> 0.2939 ms over 200 frames, test3 0.2656 -> 0.2631:
@@ -2133,9 +2197,9 @@ void rg_render_kernel(RgKernelArgs a) {
                     tile = (uint32_t)t;
                     if constexpr (RING > 0) {
                         if (use_ring) {
-                            tile = (uint32_t)t * RING;
+                            tile = (uint32_t)t * ring_g;
                             grp_next = tile + 1u;
-                            grp_end = min(tile + (uint32_t)RING, ntiles);
+                            grp_end = min(tile + ring_g, ntiles);
                         }
                     }
                     break;
@@ -2193,6 +2257,7 @@ void rg_render_kernel(RgKernelArgs a) {
                 }
                 pixel = y * a.width + x;
                 if (alive) {
+                    RG_REGION(RGR_PRIM);
                     // ray.rs:37-54 (aspect and fov_adjustment are per-frame constants)
                     double sx, sy;
                     // heavy path: the host's per-column / per-row table of the same expressions
@@ -2381,6 +2446,7 @@ void rg_render_kernel(RgKernelArgs a) {
             if (exact) occl = ~occl_full & ((1u << LB) - 1u);
             for (int l = 0; __any(l < passes); ++l) {
                 if (l < passes && (mode == MODE_CLOSEST || ((occl_full >> l) & 1u))) {
+                    RG_REGION(RGR_Q_CLOSEST);
                     Ray rq;
                     rq.o = q.o;
                     rq.d = q.d;
@@ -2400,6 +2466,7 @@ void rg_render_kernel(RgKernelArgs a) {
                 }
             }
             if (mode == MODE_SHADOW && !exact) {
+                RG_REGION(RGR_Q_SHADOW);
                 occl = ~occl_full & ((1u << LB) - 1u);  // absent slots count as done
                 trace_shadow<LB>(a, src, q.o, sb, (1u << LB) - 1u, occl);
             }
@@ -2800,7 +2867,9 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
 #ifndef RG_DEV_HEAVY_ONLY  // development builds: resource reports of the heavy kernels only
     if (!heavy) {
         if constexpr (HF) {
-            return hipErrorInvalidValue;  // light host frames run the MAXD == 0 kernels
+            // light host frames run the MAXD == 0 kernels: array-frame HF light kernels (9 spilled
+            // VGPRs) measured slower into pinned memory, 0.768 -> 0.826 ms (profiles/r06/s5)
+            return hipErrorInvalidValue;
         } else {
             if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT) {
                 // a launch on its own (not one of several frames in flight): persistent waves at full

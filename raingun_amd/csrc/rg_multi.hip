@@ -452,12 +452,14 @@ rg_status render_direct(const rg_scene *s, rg_multi_res *m, uint8_t *rgba_out, r
     // destination: the caller's buffer if page-locked, else the pinned frame
     uint8_t *dst = rg_host_is_pinned(rgba_out, frame_bytes) ? rgba_out : nullptr;
     const bool pageable = dst == nullptr;
-    // automatic (bands 0): trace-heavy scenes into a page-locked frame render in one launch per
-    // device (north star, one device's timeline 0.97 -> 0.87 ms); light scenes keep the bands,
-    // whose array kernels render a small share faster than the host-frame kernels (test1 0.27-0.31
-    // vs 0.49 ms: profiles/r04/latency_s1.json).  Only when every device can store into the frame
-    // (ADVICE r4): otherwise the banded DMA copies, which work for any page-locked buffer.
-    if (!pageable && (s->multi_bands < 0 || (s->multi_bands == 0 && rg_heavy_path(rg_make_args(s)))) &&
+    // automatic (bands 0): into a page-locked frame every device renders its share in ONE launch
+    // storing its rows over its own link -- trace-heavy scenes since round 4 (north star, one
+    // device's timeline 0.97 -> 0.87 ms), light scenes since round 6, once the light kernel's LDS
+    // tile ring flushed small launches every 4 tiles with single-tile queue slots (test1 0.29 ->
+    // 0.20 ms, the copy now overlapping the render: profiles/r06/s6; with 16-tile groups it was
+    // 0.49-0.52 ms).  Only when every device can store into the frame: otherwise the
+    // banded DMA copies, which work for any page-locked buffer.
+    if (!pageable && (s->multi_bands < 0 || (s->multi_bands == 0 && (s->multi_light_one || rg_heavy_path(rg_make_args(s))))) &&
         mapped_on_all(m, dst, frame_bytes))
         return render_direct_one(s, m, dst, stats);
     if (pageable) {

@@ -296,6 +296,14 @@ class DeviceScene:
         _abi.check(_abi.lib().rg_debug_set_multi(self.handle, int(mode), 1 if stand_in else 0, int(bands),
                                                  int(only_rank)))
 
+    def set_host_ring(self, flush_small: int = -1, group_small: int = -1, flush_big: int = -1, group_big: int = -1,
+                      multi_light_one: int = -1) -> None:
+        """Light-path host frames: LDS-ring flush size and queue group of small / big launches,
+        rg_render_multi's one launch per device for light scenes; -1 keeps a setting
+        (include/raingun_debug.h rg_debug_set_host_ring)."""
+        _abi.check(_abi.lib().rg_debug_set_host_ring(self.handle, int(flush_small), int(group_small), int(flush_big),
+                                                     int(group_big), int(multi_light_one)))
+
     def set_host_split(self, pct: int) -> None:
         """Image bands -2 (split host frames): percent of the rows rendered into device
         memory and copied by DMA beside the one-launch rest; 0 = default (raingun_debug.h)."""

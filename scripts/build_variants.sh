@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 for spec in "$@"; do
   name="${spec%%=*}"; flags="${spec#*=}"
   mkdir -p abvar/$name
-  make -s -C raingun_amd/csrc OUT=$PWD/abvar/$name/libraingun_hip.so EXTRA="$flags" >/dev/null
+  make -s -B -C raingun_amd/csrc OUT=$PWD/abvar/$name/libraingun_hip.so EXTRA="$flags" >/dev/null
   echo "$flags" > abvar/$name/flags.txt
   echo "built $name: $flags"
 done

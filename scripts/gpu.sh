@@ -17,7 +17,7 @@
 #   pcsamp:wl[:interval]          stochastic PC sampling of bench.py's timed configuration
 #   iter:lib:wl,wl..              RG_ITER_STATS counters (scripts/iter_stats.py) with a variant library
 #   shares:wl,wl..                per-rank 1/8 shares (scripts/rank_shares.sh)
-#   latency:wl,wl..               single-launch latency + rg_render_multi rehearsal (scripts/latency_probe.py)
+#   latency:wl,wl..[:lib]         single-launch latency + rg_render_multi rehearsal (scripts/latency_probe.py)
 #   py:script:args                any repo python script (args ',' -> ' '), output to TAG/<script>.out
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -93,11 +93,21 @@ PY
       rc=${PIPESTATUS[0]}; cp -r gpurun_out/shares "$O/shares" 2>/dev/null; rm -rf gpurun_out/shares
       [ $rc -eq 0 ] || exit $rc ;;
     latency)
-      timeout -k 10 300 python scripts/latency_probe.py $(sp "$a1") > "$O/lat.json" 2> "$O/lat.err" \
-        || { tail "$O/lat.err"; exit 1; }
-      tail -c 600 "$O/lat.json" | tee -a "$O/session.txt"; echo ;;
+      tag=lat${a2:+_$(basename "$(dirname "$a2")")}
+      RAINGUN_HIP_LIB=${a2:+$R/$a2} timeout -k 10 300 python scripts/latency_probe.py $(sp "$a1") > "$O/$tag.json" \
+        2> "$O/$tag.err" || { tail "$O/$tag.err"; exit 1; }
+      python - "$O/$tag.json" "$tag" <<'PY' | tee -a "$O/session.txt"
+import json, sys
+D = json.load(open(sys.argv[1]))
+for wl, d in D.items():
+    if isinstance(d, dict) and "share8_max_ms" in d:
+        m = d.get("multi_8gpu_rehearsal", {})
+        print(sys.argv[2], wl, "whole", d["whole_kernel_ms"], "share8_max", d["share8_max_ms"], "pinned1", d.get("host_pinned_1gpu_ms"),
+              "multi", m.get("projected_ms_per_step"), m.get("projected_speedup_vs_1gpu"), m.get("per_device_ms"))
+PY
+      ;;
     py)
-      base=$(basename "$a1" .py)
+      base=$(basename "$a1" .py)$(echo "${a2:+_$a2}" | tr -c 'A-Za-z0-9_\n' '_' | cut -c1-40)
       timeout -k 10 400 python "$a1" $(sp "$a2") > "$O/$base.out" 2> "$O/$base.err" \
         || { tail -20 "$O/$base.err"; exit 1; }
       tail -c 1500 "$O/$base.out" | tee -a "$O/session.txt"; echo ;;

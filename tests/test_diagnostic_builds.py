@@ -17,7 +17,8 @@ HIPCC = "/opt/rocm/bin/hipcc"
 
 
 @pytest.mark.skipif(shutil.which(HIPCC) is None and not Path(HIPCC).exists(), reason="hipcc not installed")
-@pytest.mark.parametrize("flag", ["", "-DRG_TILE_TIMES", "-DRG_WAVE_TIMES", "-DRG_ITER_STATS", "-DRG_BVH_STATS"])
+@pytest.mark.parametrize("flag", ["", "-DRG_TILE_TIMES", "-DRG_WAVE_TIMES", "-DRG_ITER_STATS", "-DRG_BVH_STATS",
+                                  "-DRG_REGION_STATS"])
 def test_diagnostic_build_compiles(flag):
     cmd = [HIPCC, "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fsyntax-only", "-Werror=return-type",
            "rg_kernels.hip"]

@@ -513,6 +513,48 @@ def test_render_multi_n_devices_stand_in(oracle_lib, example_scenes, mode, ngpus
     ds.close()
 
 
+@pytest.mark.parametrize("flush,group", [(1, 1), (2, 2), (4, 1), (8, 3), (16, 16)])
+def test_light_host_ring_settings(oracle_lib, example_scenes, flush, group):
+    """Round 6: the light path's LDS tile ring with a runtime flush size and queue group
+    (rg_debug_set_host_ring): rg_render_multi over 8 stand-in devices, each share one launch storing
+    its rows into the page-locked frame (the automatic mode for light scenes since round 6) or banded,
+    and the 1-GPU split frame, whose one-launch part is a "big" launch at 4K -- byte-exact."""
+    import copy
+
+    s = copy.copy(example_scenes["test1"])
+    s.max_recursion_depth = 5
+    w, h = 640, 357
+    o_st, o_rgba, _, o_counts, _ = _oracle(oracle_lib, s, w, h)
+    ds = DeviceScene(s)
+    ds.set_host_ring(flush_small=flush, group_small=group, flush_big=flush, group_big=group)
+    out = np.full((h, w, 4), 77, dtype=np.uint8)
+    reg = _abi.HostRegistration(out)
+    try:
+        for one in (1, 0):
+            ds.set_host_ring(multi_light_one=one)
+            ds.set_multi(0, stand_in=True, bands=0)
+            st = _abi.rg_stats()
+            out.fill(77)
+            got = ds.render_multi(w, h, 8, 8, stats=st, out=out)
+            assert np.array_equal(got, o_rgba), (one, int((got != o_rgba).any(axis=2).sum()))
+            assert st.rays.as_dict() == o_counts
+    finally:
+        reg.close()
+    ds.set_multi(0, stand_in=False, bands=0)
+    W, H = 3840, 2160
+    ref, _ = ds.render_tiles(W, H)  # device-resident (the parity tests pin it to the restatement)
+    big = np.full((H, W, 4), 5, dtype=np.uint8)
+    reg = _abi.HostRegistration(big)
+    try:
+        for _ in range(2):
+            big.fill(5)
+            ds.render_image(W, H, out=big)
+            assert np.array_equal(big, ref)
+    finally:
+        reg.close()
+        ds.close()
+
+
 @pytest.mark.parametrize("mode,bands,pinned", [(0, 2, False), (1, 2, False), (0, -1, True), (0, 2, True)])
 def test_render_multi_n_devices_reports_first_error(oracle_lib, mode, bands, pinned):
     """The NaN-distance panic (scene.rs:38) raised on several devices: the lowest
