@@ -275,9 +275,14 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     split = args.share if (world == 1 and args.share > 1) else world
     TR = args.tile_rows  # rows per interleaved row tile (rank t % N renders tile t)
     tiling = rd.tiling(args.share_rank if split != world else rank, split, TR)
-    my_rows = lib.rg_tiling_rows(H, C.byref(tiling))
+    # rank 0's share (--rank0-share R, native N-rank loop): periods of R + N - 1 tiles, the first R to
+    # rank 0 (include/raingun_frames.h rg_frames_set_root_tiles); this rank's tilings, for the counted render
+    R0 = args.rank0_share if world > 1 else 1
+    my_tilings = rd.tilings(rank, world, TR, R0) if R0 > 1 else [tiling]
+    tiling = my_tilings[0]
+    my_rows = sum(lib.rg_tiling_rows(H, C.byref(t)) for t in my_tilings)
     slot = rd.slot_rows(H, split, TR)  # equal-size gather slots (last ranks zero-padded)
-    out = torch.zeros((slot, W, 4), dtype=torch.uint8, device=dev)
+    out = torch.zeros((max(slot, my_rows), W, 4), dtype=torch.uint8, device=dev)
     # frames in flight, each on its own render stream and hardware queue (16 per
     # process, see main): 8 -- the whole frame is flat from 4 up; a rank's 1/8
     # share of the north-star frame renders in 0.481 / 0.461 / 0.439 / 0.441 ms
@@ -323,10 +328,12 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     pipe = None
     gather = world > 1 or args.rccl_rehearsal
     native = use_pipe and gather and args.backend == "nccl" and not args.python_pipeline
+    if R0 > 1 and not native:
+        raise SystemExit("--rank0-share needs the native N-rank loop (backend nccl, no --python-pipeline)")
     rccl = None
     if native:  # the per-frame loop in C++ (include/raingun_frames.h): render, ncclGather, re-interleave
         # on the library's own RCCL communicator; a failure raises (the Python loop only on request)
-        pipe = rd.NativeFramePipeline(ds, W, H, rank, world, TR, depth=F, device=dev)
+        pipe = rd.NativeFramePipeline(ds, W, H, rank, world, TR, depth=F, device=dev, root_tiles=R0)
         info = pipe.comm.info()
         if info["nranks"] != world or info["rank"] != rank:
             raise SystemExit(f"RCCL communicator {info} does not match rank {rank} of {world}")
@@ -353,11 +360,17 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         if pipe is not None:
             pipe.flush()  # the native pipeline raises on a device error of any frame
 
-    # one counted render: ray totals per class (deterministic per frame)
+    # one counted render: ray totals per class (deterministic per frame); rank 0 with a share
+    # R > 1 renders its R tilings (the native loop does them in one grouped launch)
     stats = _abi.rg_stats()
-    render(stats)
-    rays = torch.tensor([stats.rays.primary, stats.rays.shadow, stats.rays.secondary], dtype=torch.float64,
-                        device=dev)
+    counts = [0, 0, 0]
+    for t_ in my_tilings:
+        tiling = t_
+        render(stats)
+        counts = [counts[0] + stats.rays.primary, counts[1] + stats.rays.shadow, counts[2] + stats.rays.secondary]
+    tiling = my_tilings[0]
+    stats.rays.primary, stats.rays.shadow, stats.rays.secondary = counts
+    rays = torch.tensor(counts, dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(rays)
     rays = [int(x) for x in rays.tolist()]
@@ -456,7 +469,9 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
 
     if world > 1:
         via = "RCCL" if args.backend == "nccl" else f"{args.backend} (rehearsal, through host memory)"
-        parallelism = f"row-tiles x{world} (round-robin {TR}-row tiles, one {via} gather per frame to rank 0"
+        deal = f"round-robin {TR}-row tiles" if R0 == 1 else \
+            f"{TR}-row tiles in periods of {R0 + world - 1}: {R0} to rank 0, one to each other rank"
+        parallelism = f"row-tiles x{world} ({deal}, one {via} gather per frame to rank 0"
     else:
         parallelism = "one GPU (whole frame"
     if native:
@@ -487,7 +502,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
         "settle_s": args.settle_s,
         "config": {"workload": label, "width": W, "height": H, "max_recursion_depth": scene.max_recursion_depth,
                    "bodies": body_counts, "lights": len(scene.lights), "tile_rows": TR,
-                   "frames_in_flight": F, "parallelism": parallelism},
+                   "frames_in_flight": F, "parallelism": parallelism,
+                   **({"rank0_share_tiles": R0} if world > 1 else {})},
         "rays_per_frame": {"primary": rays[0], "shadow": rays[1], "secondary": rays[2], "total": rays_per_frame},
         "roofline": roof,
         "roofline_hbm": roof_hbm,
@@ -584,11 +600,13 @@ def multi_rehearsal(ds, W: int, H: int, one_gpu_ms: float, args, n: int = 8, bud
             ds.set_multi(0, stand_in=True, bands=0, only_rank=r)
             for _ in range(2):
                 ds.render_multi(W, H, n, 8, out=buf)
-            k, t0 = 0, time.perf_counter()
-            while k < 5 or (time.perf_counter() - t0 < budget_s and k < args.steps):
+            # the median call: one host hiccup (the box's other work) must not decide a device's time
+            times, t0 = [], time.perf_counter()
+            while len(times) < 5 or (time.perf_counter() - t0 < budget_s and len(times) < args.steps):
+                t1 = time.perf_counter()
                 ds.render_multi(W, H, n, 8, out=buf)
-                k += 1
-            per_rank.append((time.perf_counter() - t0) / k * 1e3)
+                times.append(time.perf_counter() - t1)
+            per_rank.append(float(np.median(times)) * 1e3)
             if split:
                 t = _abi.rg_tiling(8, n, r)
                 rows = lib.rg_tiling_rows(H, C.byref(t))
@@ -683,6 +701,9 @@ def main() -> None:
                     help="rows per interleaved row tile of the N-way split (8: the slowest of 8 shares is 2-4 %% "
                          "faster than with 16, profiles/r01/bench_rank_shares.txt)")
     ap.add_argument("--share-rank", type=int, default=0, help="diagnostic: which rank's share --share times")
+    ap.add_argument("--rank0-share", type=int, default=1,
+                    help="N > 1: tiles of rank 0 per period of R + N - 1 (rank 0's rows never cross xGMI; "
+                         "1 = round robin; include/raingun_frames.h rg_frames_set_root_tiles)")
     ap.add_argument("--depth", type=int, default=None, help="diagnostic: override the workload's recursion depth")
     ap.add_argument("--lane-depth", type=int, default=None,
                     help="diagnostic: rays at recursion depth >= this walk the BVH per lane (rg_debug_set_lane_depth)")

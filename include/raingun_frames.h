@@ -50,6 +50,16 @@ void rg_frames_destroy(rg_frames *frames);
  * same either way (a batch cut short by rg_frames_flush is gathered then). */
 rg_status rg_frames_set_batch(rg_frames *frames, int32_t batch);
 
+/* Rank 0's share: the frame's tile_rows-row tiles are dealt in periods of
+ * root_tiles + world - 1 -- the first root_tiles of each period to rank 0, then
+ * one to each other rank (1, the default: the round robin tile t -> rank t %
+ * world).  Rank 0's rows never cross the interconnect, so a larger share
+ * shrinks every other rank's part of each gather (and the root's receive
+ * volume) at the cost of more rendering on rank 0.  Every rank must set the
+ * same value, before the first rg_frames_step.  The assembled frame is the
+ * same for every value. */
+rg_status rg_frames_set_root_tiles(rg_frames *frames, int32_t root_tiles);
+
 /* Enqueue one frame (asynchronous: returns once its work is on the streams). */
 rg_status rg_frames_step(rg_frames *frames);
 

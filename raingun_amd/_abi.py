@@ -146,7 +146,7 @@ DEBUG_SYMBOLS = ("rg_debug_set_path", "rg_debug_set_bvh", "rg_debug_bvh_info", "
                  "rg_debug_counter_words")
 # include/raingun_frames.h
 FRAMES_SYMBOLS = ("rg_frames_create", "rg_frames_destroy", "rg_frames_step", "rg_frames_flush", "rg_frames_image",
-                  "rg_frames_read_image", "rg_frames_status", "rg_frames_set_batch", "rg_comm_id_bytes",
+                  "rg_frames_read_image", "rg_frames_status", "rg_frames_set_batch", "rg_frames_set_root_tiles", "rg_comm_id_bytes",
                   "rg_comm_unique_id", "rg_comm_init_rank", "rg_comm_info", "rg_comm_destroy", "rg_comm_gather_fn")
 PATH_AUTO, PATH_LIGHT, PATH_HEAVY = -1, 0, 1
 
@@ -260,6 +260,9 @@ def _declare(lib: C.CDLL) -> None:
     if hasattr(lib, "rg_frames_set_batch"):  # absent from pre-round-3 builds
         lib.rg_frames_set_batch.restype = C.c_int32
         lib.rg_frames_set_batch.argtypes = [C.c_void_p, C.c_int32]
+    if hasattr(lib, "rg_frames_set_root_tiles"):  # absent from pre-round-6 builds
+        lib.rg_frames_set_root_tiles.restype = C.c_int32
+        lib.rg_frames_set_root_tiles.argtypes = [C.c_void_p, C.c_int32]
     if hasattr(lib, "rg_comm_init_rank"):  # absent from pre-round-4 builds
         lib.rg_comm_id_bytes.restype = C.c_int32
         lib.rg_comm_unique_id.restype = C.c_int32

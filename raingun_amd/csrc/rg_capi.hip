@@ -276,12 +276,14 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
                           uint8_t *rgba_dev, float *rgb_dev, hipStream_t st, unsigned long long *snap,
                           rg_launch_ctx **ctx_out, bool timed, uint32_t *tile_flags, uint32_t frame_seq,
                           const uint32_t *cancel, uint32_t tile_wlog, bool host_frame, bool pipelined,
-                          uint32_t tile_first, uint32_t tile_count, bool image_rows) {
+                          uint32_t tile_first, uint32_t tile_count, bool image_rows, uint32_t tile_group) {
     if (tile_wlog < 3 || tile_wlog > 6) return RG_ERR_INVALID_ARGUMENT;
     if (image_rows && (!host_frame || rgb_dev)) return RG_ERR_INVALID_ARGUMENT;
     if (!s || !rgba_dev || width == 0 || height == 0 || !tiling_valid(tiling)) return RG_ERR_INVALID_ARGUMENT;
+    if (tile_group < 1 || tiling->tile_offset + tile_group > tiling->tile_stride + (tile_group == 1 ? 1u : 0u))
+        return RG_ERR_INVALID_ARGUMENT;
     if (width < height) return RG_ERR_PORTRAIT;  // ray.rs:42
-    const uint32_t sel_rows = rg_tiling_rows(height, tiling);  // every selected tile
+    const uint32_t sel_rows = rg_tiling_rows_grouped(height, tiling, tile_group);  // every selected tile
     const uint32_t sel_tiles = sel_rows / tiling->tile_rows;
     if (tile_first > sel_tiles) return RG_ERR_INVALID_ARGUMENT;
     const uint32_t out_rows = std::min(sel_tiles - tile_first, tile_count) * tiling->tile_rows;
@@ -301,6 +303,7 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
     a.tile_rows = tiling->tile_rows;
     a.tile_stride = tiling->tile_stride;
     a.tile_offset = tiling->tile_offset;
+    a.tile_group = tile_group;
     a.tile_base = tile_first;
     a.out_rows = out_rows;
     a.aspect = (double)width / (double)height;
@@ -392,7 +395,7 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
         const size_t ntiles = (size_t)rg_tile_count(a);
         const rg_launch_ctx::PermKey key{width, height, tiling->tile_rows, tiling->tile_stride, tiling->tile_offset,
                                          tile_first, out_rows, tile_wlog, s->max_depth, (uint32_t)s->n_lights,
-                                         a.fov_adjustment, s->mats};
+                                         tile_group, a.fov_adjustment, s->mats};
         if (!(cx->perm_valid && cx->perm_key == key) && ntiles > cx->tile_cap) {
             if (cx->tile_cost) (void)hipFree(cx->tile_cost);
             if (cx->tile_perm) (void)hipFree(cx->tile_perm);
@@ -612,6 +615,15 @@ void rg_sync_settings(rg_scene *dst, const rg_scene *src) {
     dst->ring_group_big = src->ring_group_big;
 }
 
+uint32_t rg_tiling_rows_grouped(uint32_t height, const rg_tiling *t, uint32_t group) {
+    if (!tiling_valid(t) || height == 0 || group < 1 || (group > 1 && t->tile_offset + group > t->tile_stride)) return 0;
+    const uint32_t tiles = (height + t->tile_rows - 1) / t->tile_rows;
+    // per stride of image tiles: tiles offset .. offset + group - 1 (group 1: the round robin)
+    const uint32_t full = tiles / t->tile_stride, rem = tiles % t->tile_stride;
+    const uint32_t last = rem > t->tile_offset ? std::min(group, rem - t->tile_offset) : 0u;
+    return (full * group + last) * t->tile_rows;
+}
+
 extern "C" {
 
 int32_t rg_abi_version(void) { return RG_ABI_VERSION; }
@@ -640,12 +652,7 @@ int32_t rg_device_count(void) {
     return n;
 }
 
-uint32_t rg_tiling_rows(uint32_t height, const rg_tiling *t) {
-    if (!tiling_valid(t) || height == 0) return 0;
-    uint32_t tiles = (height + t->tile_rows - 1) / t->tile_rows;
-    uint32_t mine = tiles > t->tile_offset ? (tiles - t->tile_offset + t->tile_stride - 1) / t->tile_stride : 0;
-    return mine * t->tile_rows;
-}
+uint32_t rg_tiling_rows(uint32_t height, const rg_tiling *t) { return rg_tiling_rows_grouped(height, t, 1); }
 
 rg_status rg_scene_create(const rg_scene_desc *d, int32_t device, rg_scene **out) {
     if (!d || !out) return RG_ERR_INVALID_ARGUMENT;

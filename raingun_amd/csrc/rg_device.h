@@ -135,6 +135,10 @@ struct RgKernelArgs {
     // frame
     uint32_t width, height;
     uint32_t tile_rows, tile_stride, tile_offset, out_rows;
+    // selected tiles in groups of tile_group consecutive image tiles (1: the plain round robin):
+    // selected tile i is image tile (i / group) * stride + offset + i % group -- rank 0's larger
+    // share of the N-rank frame loop (rg_frames_set_root_tiles)
+    uint32_t tile_group;
     uint32_t tile_base;      // the launch renders selected tiles tile_base, tile_base + 1, ... (output row 0 = its first row)
     double fov_adjustment;   // tan(fov.to_radians() / 2), ray.rs:45 (host libm)
     double aspect;           // width / height, ray.rs:43

@@ -49,19 +49,24 @@ __global__ __launch_bounds__(256) void rg_pack_rgb_kernel(const uint32_t *rgba, 
     }
 }
 
-// Image row y lives in tile t = y / T, dealt to rank t % world as that rank's
-// (t / world)-th tile: row (t / world) * T + y % T of its part (distributed.py
-// assemble).  Rank 0's rows come from root_part (RGBA), the others' from
-// their packed slots (slot_bytes apart).  4 pixels per thread.
+// Image row y lives in tile t = y / T.  The tiles are dealt in periods of
+// P = root + world - 1: the first `root` tiles of each period to rank 0, then one
+// to each other rank (root = 1: the round robin t -> rank t % world).  Tile t is
+// that rank's (t / P * root + t % P)-th (rank 0) or (t / P)-th tile (the others):
+// its row of the part is that index * T + y % T (distributed.py assemble).  Rank
+// 0's rows come from root_part (RGBA), the others' from their packed slots
+// (slot_bytes apart).  4 pixels per thread.
 __global__ __launch_bounds__(256) void rg_reinterleave_kernel(const uint8_t *gathered, const uint32_t *root_part,
                                                               uint32_t *image, uint32_t width, uint32_t height,
-                                                              uint32_t tile_rows, uint32_t world, size_t slot_bytes) {
+                                                              uint32_t tile_rows, uint32_t world, uint32_t root,
+                                                              size_t slot_bytes) {
     const uint32_t y = blockIdx.y;
     const uint32_t x0 = (blockIdx.x * 256u + threadIdx.x) * 4u;
     if (y >= height || x0 >= width) return;
-    const uint32_t t = y / tile_rows;
-    const uint32_t r = t % world;
-    const uint32_t src_row = (t / world) * tile_rows + (y - t * tile_rows);
+    const uint32_t t = y / tile_rows, P = root + world - 1u;
+    const uint32_t p = t / P, j = t - p * P;
+    const uint32_t r = j < root ? 0u : j - root + 1u;
+    const uint32_t src_row = (r == 0u ? p * root + j : p) * tile_rows + (y - t * tile_rows);
     uint32_t *dst = image + (size_t)y * width + x0;
     const size_t src_px = (size_t)src_row * width + x0;
     if (r == 0) {
@@ -102,11 +107,11 @@ hipError_t rg_launch_pack_rgb(const void *rgba, void *rgb, size_t npx, hipStream
 
 hipError_t rg_launch_reinterleave(const void *gathered, const void *root_part, void *image, uint32_t width,
                                   uint32_t height, uint32_t tile_rows, uint32_t world, size_t slot_bytes,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, uint32_t root) {
     dim3 grid((((width + 3u) / 4u) + 255u) / 256u, height);
     hipLaunchKernelGGL(rg_reinterleave_kernel, grid, dim3(256), 0, stream, static_cast<const uint8_t *>(gathered),
                        static_cast<const uint32_t *>(root_part), static_cast<uint32_t *>(image), width, height,
-                       tile_rows, world, slot_bytes);
+                       tile_rows, world, root, slot_bytes);
     return hipGetLastError();
 }
 
@@ -118,6 +123,8 @@ struct rg_frames {
     size_t part_bytes = 0;   // RGBA part of a frame
     size_t slot_bytes = 0;   // packed RGB part: what each rank sends (rg_packed_slot_bytes)
     rg_tiling tiling{};
+    uint32_t root = 1;          // tiles of rank 0 per period (rg_frames_set_root_tiles)
+    size_t root_part_rows = 0;  // rows of rank 0's part
     void *comm = nullptr;
     rg_gather_fn gather = nullptr;
     std::vector<hipStream_t> render;
@@ -197,6 +204,7 @@ rg_status rg_frames_create(const rg_scene *scene, uint32_t width, uint32_t heigh
     f->tiling = rg_tiling{tile_rows, (uint32_t)world, (uint32_t)rank};
     const uint32_t tiles = (height + tile_rows - 1) / tile_rows;
     f->slot_rows = (tiles + (uint32_t)world - 1) / (uint32_t)world * tile_rows;  // equal on every rank
+    f->root_part_rows = f->slot_rows;
     f->part_bytes = (size_t)f->slot_rows * width * 4;
     f->slot_bytes = rg_packed_slot_bytes(f->slot_rows, width);
     bool good = true;
@@ -268,7 +276,8 @@ rg_status issue_gather(rg_frames *f, int b0, int n) {
         const int b = b0 + h;
         if (f->rank == 0) {
             if (!ok(rg_launch_reinterleave(static_cast<uint8_t *>(recv) + (size_t)h * f->slot_bytes, f->parts[b],
-                                           f->image[b], f->w, f->h, f->T, (uint32_t)f->world, count, f->side)) ||
+                                           f->image[b], f->w, f->h, f->T, (uint32_t)f->world, count, f->side,
+                                           f->root)) ||
                 !ok(hipEventRecord(f->done[b], f->side)))
                 return RG_ERR_DEVICE;
         } else if (!ok(hipEventRecord(f->done[b], f->comm_stream))) {
@@ -287,6 +296,34 @@ extern "C" {
 // raingun_debug.h: a gather that does nothing (host-overhead probes of the frame loop)
 int rg_debug_gather_noop(const void *, void *, size_t, int, int, void *, void *) { return 0; }
 
+rg_status rg_frames_set_root_tiles(rg_frames *f, int32_t root_tiles) {
+    if (!f || root_tiles < 1 || root_tiles > 64 || f->k != 0) return RG_ERR_INVALID_ARGUMENT;
+    if (f->world == 1) return root_tiles == 1 ? RG_OK : RG_ERR_INVALID_ARGUMENT;
+    const uint32_t R = (uint32_t)root_tiles, P = R + (uint32_t)f->world - 1u;
+    // rank 0: R consecutive tiles per period; rank r > 0: tile R + r - 1 of each period
+    f->root = R;
+    f->tiling = f->rank == 0 ? rg_tiling{f->T, P, 0u} : rg_tiling{f->T, P, R + (uint32_t)f->rank - 1u};
+    const rg_tiling t1{f->T, P, R};  // rank 1 holds the most tiles of the other ranks
+    const rg_tiling t0{f->T, P, 0u};
+    const uint32_t slot_rows = rg_tiling_rows_grouped(f->h, &t1, 1);
+    const size_t root_rows = rg_tiling_rows_grouped(f->h, &t0, R);
+    const size_t part_rows = f->rank == 0 ? std::max<size_t>(root_rows, slot_rows) : slot_rows;
+    if (part_rows * f->w * 4 > f->part_bytes) {  // rank 0's part grew: new part buffers
+        for (void *&p : f->parts) {
+            (void)hipFree(p);
+            p = nullptr;
+        }
+        const size_t bytes = std::max(part_rows * f->w * 4, rg_packed_slot_bytes(slot_rows, f->w) * 2);
+        for (void *&p : f->parts)
+            if (!ok(hipMalloc(&p, bytes)) || !ok(hipMemset(p, 0, bytes))) return RG_ERR_OUT_OF_MEMORY;
+        f->part_bytes = part_rows * f->w * 4;
+    }
+    f->slot_rows = slot_rows;  // smaller than before: the send / receive buffers stay large enough
+    f->slot_bytes = rg_packed_slot_bytes(slot_rows, f->w);
+    f->root_part_rows = root_rows;
+    return RG_OK;
+}
+
 rg_status rg_frames_set_batch(rg_frames *f, int32_t batch) {
     if (!f || batch < 1 || batch > 2 || f->depth % batch != 0 || f->k != 0) return RG_ERR_INVALID_ARGUMENT;
     f->batch = batch;
@@ -298,8 +335,10 @@ rg_status rg_frames_step(rg_frames *f) {
     const int b = (int)(f->k % (unsigned long long)f->depth);
     hipStream_t rs = f->render[b];
     if (f->k >= (unsigned long long)f->depth && !ok(hipStreamWaitEvent(rs, f->done[b], 0))) return RG_ERR_DEVICE;
-    rg_status st = rg_render_tiles_pipelined(f->scene, f->w, f->h, &f->tiling, static_cast<uint8_t *>(f->parts[b]),
-                                             nullptr, rs);
+    // (one of several frames in flight: the heavy path sizes its grid for throughput)
+    rg_status st = rg_launch_tiles(f->scene, f->w, f->h, &f->tiling, static_cast<uint8_t *>(f->parts[b]), nullptr, rs,
+                                   nullptr, nullptr, false, nullptr, 0, nullptr, 3, false, true, 0, 0xFFFFFFFFu, false,
+                                   f->rank == 0 ? f->root : 1u);
     if (st != RG_OK) return st;
     // off the root the part travels packed (3 B per pixel) in its batch's send buffer;
     // the root's own part is read in place

@@ -33,12 +33,14 @@ struct rg_launch_ctx {
     // the launch the cached tile_perm was made for: the order is a function of
     // the frame geometry and the scene (probe rays, materials, lights, depth)
     struct PermKey {
-        uint32_t width, height, tile_rows, tile_stride, tile_offset, tile_base, out_rows, tile_wlog, max_depth, n_lights;
+        uint32_t width, height, tile_rows, tile_stride, tile_offset, tile_base, out_rows, tile_wlog, max_depth, n_lights,
+            tile_group;
         double fov;
         const void *mats;
         bool operator==(const PermKey &o) const {
             return width == o.width && height == o.height && tile_rows == o.tile_rows && tile_stride == o.tile_stride &&
                    tile_offset == o.tile_offset && tile_base == o.tile_base && out_rows == o.out_rows &&
+                   tile_group == o.tile_group &&
                    tile_wlog == o.tile_wlog && max_depth == o.max_depth &&
                    n_lights == o.n_lights && fov == o.fov && mats == o.mats;
         }
@@ -231,7 +233,13 @@ rg_status rg_launch_tiles(const rg_scene *s, uint32_t width, uint32_t height, co
                           // rgba_dev / rgb_dev pointing at tile_first's first row
                           uint32_t tile_first = 0, uint32_t tile_count = 0xFFFFFFFFu,
                           // host_frame only: rgba_dev is the whole image, pixels go to their image rows
-                          bool image_rows = false);
+                          bool image_rows = false,
+                          // groups of tile_group consecutive image tiles per stride (RgKernelArgs::tile_group)
+                          uint32_t tile_group = 1);
+
+// Rows a tiling selects when its tiles come in groups of `group` consecutive image tiles per
+// stride (group 1: rg_tiling_rows); 0 for an invalid tiling or group (offset + group > stride).
+uint32_t rg_tiling_rows_grouped(uint32_t height, const rg_tiling *t, uint32_t group);
 
 // Ray counts and status of a counter snapshot (stats nullable).
 rg_status rg_snap_status(const unsigned long long *snap, rg_stats *stats);

@@ -1324,7 +1324,10 @@ struct FrameStack<0> {
 
 __device__ __forceinline__ uint32_t out_row_to_y(const RgKernelArgs &a, uint32_t orow) {
     uint32_t tl = orow / a.tile_rows, r = orow - tl * a.tile_rows;
-    unsigned long long y = ((unsigned long long)(tl + a.tile_base) * a.tile_stride + a.tile_offset) * a.tile_rows + r;
+    const unsigned long long i = (unsigned long long)(tl + a.tile_base);
+    const unsigned long long ti = a.tile_group > 1u ? (i / a.tile_group) * a.tile_stride + a.tile_offset + i % a.tile_group
+                                                    : i * a.tile_stride + a.tile_offset;
+    unsigned long long y = ti * a.tile_rows + r;
     return y >= a.height ? 0xFFFFFFFFu : (uint32_t)y;
 }
 

@@ -48,7 +48,7 @@
 // rg_frames.hip: parts travel as packed RGB (3 B per pixel); device 0 reads its own part in place
 hipError_t rg_launch_reinterleave(const void *gathered, const void *root_part, void *image, uint32_t width,
                                   uint32_t height, uint32_t tile_rows, uint32_t world, size_t slot_bytes,
-                                  hipStream_t stream);
+                                  hipStream_t stream, uint32_t root = 1);
 hipError_t rg_launch_pack_rgb(const void *rgba, void *rgb, size_t npx, hipStream_t stream);
 size_t rg_packed_slot_bytes(uint32_t slot_rows, uint32_t width);
 

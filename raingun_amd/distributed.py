@@ -8,6 +8,12 @@ ranks' buffers are zero-padded so every rank sends the same byte count), and
 ONE gather (torch.distributed; backend "nccl" is RCCL over xGMI) brings the
 buffers to rank 0, which re-interleaves them into image order.
 
+Rank 0's share (`root` > 1, rg_frames_set_root_tiles): the tiles are dealt in
+periods of root + world - 1 -- the first `root` of each period to rank 0, then
+one to each other rank.  Rank 0's rows never cross the interconnect, so every
+other rank's part of the gather shrinks; rank 0's own part is larger than the
+equal-size slots of the others and is not sent.
+
 There is no other collective on the data path.
 """
 from __future__ import annotations
@@ -30,8 +36,36 @@ def slot_rows(height: int, world: int, tile_rows: int = TILE_ROWS) -> int:
     return tiles_per_rank(height, world, tile_rows) * tile_rows
 
 
-def rank_tiles(height: int, rank: int, world: int, tile_rows: int = TILE_ROWS) -> list:
-    return list(range(rank, n_tiles(height, tile_rows), world))
+def rank_tiles(height: int, rank: int, world: int, tile_rows: int = TILE_ROWS, root: int = 1) -> list:
+    """Image tiles of `rank`, in the order its part holds them."""
+    n = n_tiles(height, tile_rows)
+    if root == 1:
+        return list(range(rank, n, world))
+    P = root + world - 1
+    if rank == 0:
+        return [t for t in range(n) if t % P < root]
+    return list(range(root + rank - 1, n, P))
+
+
+def root_slot_rows(height: int, world: int, tile_rows: int = TILE_ROWS, root: int = 1) -> int:
+    """Rows of the other ranks' equal-size gather slots with rank 0's share `root` (root 1: slot_rows)."""
+    if root == 1 or world == 1:
+        return slot_rows(height, world, tile_rows)
+    return len(rank_tiles(height, 1, world, tile_rows, root)) * tile_rows
+
+
+def tilings(rank: int, world: int, tile_rows: int = TILE_ROWS, root: int = 1) -> list:
+    """The rg_tiling(s) whose selected tiles, interleaved one by one, make up `rank`'s part: ONE for
+    every rank but rank 0 with root > 1, whose `root` tiles per period are `root` strided tilings
+    (the native loop renders them in one launch: rg_frames.hip, RgKernelArgs::tile_group)."""
+    from ._abi import rg_tiling
+
+    if root == 1:
+        return [rg_tiling(tile_rows, world, rank)]
+    P = root + world - 1
+    if rank == 0:
+        return [rg_tiling(tile_rows, P, j) for j in range(root)]
+    return [rg_tiling(tile_rows, P, root + rank - 1)]
 
 
 def tiling(rank: int, world: int, tile_rows: int = TILE_ROWS):
@@ -41,12 +75,26 @@ def tiling(rank: int, world: int, tile_rows: int = TILE_ROWS):
     return rg_tiling(tile_rows, world, rank)
 
 
-def assemble(gathered, height: int, world: int, tile_rows: int = TILE_ROWS):
+def assemble(gathered, height: int, world: int, tile_rows: int = TILE_ROWS, root: int = 1):
     """Re-interleave the per-rank buffers into image order.
 
     `gathered` is a list (index = rank) of (slot_rows, W, C) tensors or arrays,
-    or one stacked (world, slot_rows, W, C) tensor/array.  Returns (height, W, C)."""
+    or one stacked (world, slot_rows, W, C) tensor/array.  Returns (height, W, C).
+    With rank 0's share `root` > 1, gathered[0] is rank 0's own (larger) part."""
     import numpy as np
+
+    if root > 1 and world > 1:
+        T = tile_rows
+        out = None
+        for r in range(world):
+            part = gathered[r]
+            for j, t in enumerate(rank_tiles(height, r, world, T, root)):
+                rows = part[j * T:(j + 1) * T][:height - t * T]
+                if out is None:
+                    out = (np.empty((height,) + tuple(part.shape[1:]), dtype=part.dtype) if isinstance(part, np.ndarray)
+                           else part.new_empty((height,) + tuple(part.shape[1:])))
+                out[t * T:t * T + rows.shape[0]] = rows
+        return out
 
     is_np = isinstance(gathered, np.ndarray) or (isinstance(gathered, (list, tuple)) and
                                                  isinstance(gathered[0], np.ndarray))
@@ -81,11 +129,37 @@ def gather_buffers(part, world: int):
     return list(big.unbind(0))
 
 
+def _root_part(render_tiles, height: int, world: int, tile_rows: int, root: int):
+    """Rank 0's part with share `root` > 1: its `root` strided tilings rendered and interleaved
+    tile by tile (local tile p * root + s = tile p of tiling s)."""
+    T, subs = tile_rows, [render_tiles(t) for t in tilings(0, world, tile_rows, root)]
+    n = len(rank_tiles(height, 0, world, T, root))
+    part = subs[0].new_zeros((n * T,) + tuple(subs[0].shape[1:]))
+    for i in range(n):
+        p, s = divmod(i, root)
+        part[i * T:(i + 1) * T] = subs[s][p * T:(p + 1) * T]
+    return part
+
+
 def render_frame(render_tiles: Callable[[object], object], height: int, rank: int, world: int,
-                 tile_rows: int = TILE_ROWS, group=None, out=None, gather_bufs=None):
+                 tile_rows: int = TILE_ROWS, group=None, out=None, gather_bufs=None, root: int = 1):
     """Render this rank's tiles with `render_tiles(tiling) -> (slot_rows, W, 4)
     tensor` and gather the frame to rank 0.  Returns the (height, W, 4) frame on
-    rank 0 and None on the other ranks."""
+    rank 0 and None on the other ranks.  root > 1: rank 0's share (module doc);
+    render_tiles then returns that tiling's rows, zero-padded to root_slot_rows."""
+    if root > 1 and world > 1:
+        import torch.distributed as dist
+
+        slot = root_slot_rows(height, world, tile_rows, root)
+        if rank == 0:
+            mine = _root_part(render_tiles, height, world, tile_rows, root)
+            dummy = mine.new_zeros((slot,) + tuple(mine.shape[1:]))  # rank 0's slot of the gather is not read
+            bufs = [dummy.new_empty(dummy.shape) for _ in range(world)]
+            dist.gather(dummy, bufs, dst=0, group=group)
+            return assemble([mine] + bufs[1:], height, world, tile_rows, root)
+        part = render_tiles(tilings(rank, world, tile_rows, root)[0])[:slot]
+        dist.gather(part.contiguous(), None, dst=0, group=group)
+        return None
     part = render_tiles(tiling(rank, world, tile_rows))
     if world == 1:
         return part[:height]
@@ -324,7 +398,7 @@ class NativeFramePipeline:
     library's own (RcclComm, over the ranks of `group`); failures raise."""
 
     def __init__(self, scene, width: int, height: int, rank: int, world: int, tile_rows: int = TILE_ROWS,
-                 depth: int = 4, group=None, device=None):
+                 depth: int = 4, group=None, device=None, root_tiles: int = 1):
         import ctypes as C
 
         import torch
@@ -347,6 +421,8 @@ class NativeFramePipeline:
                                         self.comm.handle, C.c_void_p(self.comm.gather_fn), C.byref(h))
         _abi.check(st, "rg_frames_create")
         self._h = h
+        if root_tiles != 1:  # rank 0's share (include/raingun_frames.h rg_frames_set_root_tiles)
+            _abi.check(self._lib.rg_frames_set_root_tiles(h, int(root_tiles)), "rg_frames_set_root_tiles")
 
     def step(self, render=None):
         from . import _abi

@@ -76,6 +76,78 @@ def test_assemble_index_math():
     assert tiles == 7 and rd.tiles_per_rank(H, world, T) == 3
 
 
+@pytest.mark.parametrize("world,root", [(2, 2), (3, 2), (3, 4), (8, 2), (8, 3)])
+def test_root_share_index_math(world, root):
+    """Rank 0's share: periods of root + world - 1 tiles, the first `root` to
+    rank 0.  Every image tile belongs to exactly one rank, the other ranks' slots are equal up to
+    one tile, rank 0's tilings interleave to its tile list, and assemble() restores the image."""
+    H, T = 203, 8
+    tiles = rd.n_tiles(H, T)
+    owned = sorted(t for r in range(world) for t in rd.rank_tiles(H, r, world, T, root))
+    assert owned == list(range(tiles))
+    counts = [len(rd.rank_tiles(H, r, world, T, root)) for r in range(1, world)]
+    assert max(counts) - min(counts) <= 1 and rd.root_slot_rows(H, world, T, root) == max(counts) * T
+    P = root + world - 1
+    ts = rd.tilings(0, world, T, root)
+    assert [(t.tile_stride, t.tile_offset) for t in ts] == [(P, j) for j in range(root)]
+    inter = []
+    for p in range(tiles // P + 1):
+        inter += [p * P + t.tile_offset for t in ts if p * P + t.tile_offset < tiles]
+    assert inter == rd.rank_tiles(H, 0, world, T, root)
+    img = np.arange(H)[:, None, None].repeat(3, 1).repeat(1, 2)
+    parts = []
+    for r in range(world):
+        mine = rd.rank_tiles(H, r, world, T, root)
+        rows = len(mine) * T if r == 0 else rd.root_slot_rows(H, world, T, root)
+        buf = np.full((rows, 3, 1), -1)
+        for j, t in enumerate(mine):
+            blk = img[t * T:(t + 1) * T]
+            buf[j * T:j * T + blk.shape[0]] = blk
+        parts.append(buf)
+    assert np.array_equal(rd.assemble(parts, H, world, T, root), img)
+    assert torch.equal(rd.assemble([torch.from_numpy(p) for p in parts], H, world, T, root), torch.from_numpy(img))
+
+
+def _root_worker(rank, world, root, port, W, H, T, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from raingun_amd.scene import SceneDesc, load_scene
+        from pathlib import Path
+        g = Path(__file__).resolve().parent / "golden"
+        desc = SceneDesc(load_scene(g / "examples" / "test2.yml", texture_root=g))
+        slot = max(rd.root_slot_rows(H, world, T, root), len(rd.rank_tiles(H, 0, world, T, root)) * T)
+
+        def render_tiles(t):
+            st, rgba, _, _, _ = oracle.render(desc, W, H, t.tile_rows, t.tile_stride, t.tile_offset, threads=2)
+            assert st == 0
+            buf = np.zeros((slot, W, 4), np.uint8)
+            buf[:rgba.shape[0]] = rgba
+            return torch.from_numpy(buf)
+
+        frame = rd.render_frame(render_tiles, H, rank, world, T, root=root)
+        if rank == 0:
+            np.save(out_path, frame.numpy())
+        else:
+            assert frame is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,root,T", [(2, 2, 8), (3, 3, 16)])
+def test_gloo_gather_root_share(oracle_lib, example_scenes, world, root, T, tmp_path):
+    """World 2/3 over gloo with rank 0's share > 1: rank 0 renders its `root` tiles per period (its
+    strided tilings, interleaved), the others one each; ONE gather of the others' equal slots;
+    the assembled frame equals the 1-rank render."""
+    from raingun_amd.scene import SceneDesc
+    W, H = 160, 117
+    _, whole, _, _, _ = oracle_lib.render(SceneDesc(example_scenes["test2"]), W, H)
+    out = str(tmp_path / "frame.npy")
+    mp.spawn(_root_worker, args=(world, root, _free_port(), W, H, T, out), nprocs=world, join=True)
+    assert np.array_equal(np.load(out), whole)
+
+
 def _pipe_worker(rank, world, port, W, H, T, K, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -89,15 +89,19 @@ def _fake_gather(world, others, calls):
     return GATHER_FN(gather)
 
 
-@pytest.mark.parametrize("world,w,h,T,depth,batch", [(2, 320, 243, 8, 3, 1), (3, 256, 144, 16, 2, 2),
-                                                     (8, 640, 357, 8, 4, 2), (8, 640, 357, 8, 4, 1),
-                                                     (8, 97, 61, 8, 1, 1), (2, 64, 40, 8, 8, 0)])
-def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, depth, batch):
+@pytest.mark.parametrize("world,w,h,T,depth,batch,root", [(2, 320, 243, 8, 3, 1, 1), (3, 256, 144, 16, 2, 2, 1),
+                                                          (8, 640, 357, 8, 4, 2, 1), (8, 640, 357, 8, 4, 1, 1),
+                                                          (8, 97, 61, 8, 1, 1, 1), (2, 64, 40, 8, 8, 0, 1),
+                                                          (8, 640, 357, 8, 4, 2, 2), (3, 320, 243, 8, 3, 1, 3),
+                                                          (2, 256, 149, 16, 4, 2, 4), (8, 97, 61, 8, 2, 0, 2)])
+def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, depth, batch, root):
     """The N > 1 native loop on one GPU: rank 0 of `world` ranks,
     the other ranks' parts (tiling {T, world, r}) pre-rendered and delivered by
     a stand-in gather.  The re-interleave, the slot offsets and the padding of
     heights that are not a multiple of T all run; every frame equals the
-    one-shot render byte for byte."""
+    one-shot render byte for byte.  root > 1: rank 0 renders
+    `root` consecutive tiles of every period of root + world - 1 in one launch
+    (grouped tiling), the others tile root + r - 1 of each period."""
     import torch
 
     from raingun_amd import _abi
@@ -105,12 +109,13 @@ def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, de
     ds = DeviceScene(example_scenes["test1"])
     ref = ds.render_image(w, h)
     lib = _abi.lib()
-    slot = rd.slot_rows(h, world, T)
+    slot = rd.root_slot_rows(h, world, T, root)
     slot_bytes = (slot * w * 3 + 15) // 16 * 16  # off the root a part travels as packed RGB (rg_frames.hip)
-    parts = [torch.zeros((slot, w, 4), dtype=torch.uint8, device="cuda") for _ in range(world)]
+    parts = [torch.zeros((max(slot, 8), w, 4), dtype=torch.uint8, device="cuda") for _ in range(world)]
     others = [torch.zeros(slot_bytes, dtype=torch.uint8, device="cuda") for _ in range(world)]
     for r in range(1, world):
-        t = _abi.rg_tiling(T, world, r)
+        t = rd.tilings(r, world, T, root)[0]
+        assert lib.rg_tiling_rows(h, C.byref(t)) <= slot
         _abi.check(lib.rg_render_tiles_async(ds.handle, w, h, C.byref(t), C.c_void_p(parts[r].data_ptr()), None,
                                              None, None))
         torch.cuda.synchronize()
@@ -123,6 +128,8 @@ def test_native_pipeline_world_n_reinterleave(example_scenes, world, w, h, T, de
                                     C.byref(hdl)))
     if batch:  # 0: the default (two frames per gather at world > 1 with an even depth)
         _abi.check(lib.rg_frames_set_batch(hdl, batch))
+    if root != 1:
+        _abi.check(lib.rg_frames_set_root_tiles(hdl, root))
     out = np.empty((h, w, 4), np.uint8)
     b = batch or (2 if depth % 2 == 0 else 1)
     for k in range(2 * depth + 1):

@@ -542,7 +542,7 @@ def test_light_host_ring_settings(oracle_lib, example_scenes, flush, group):
         reg.close()
     ds.set_multi(0, stand_in=False, bands=0)
     W, H = 3840, 2160
-    ref, _ = ds.render_tiles(W, H)  # device-resident (the parity tests pin it to the restatement)
+    ref, _ = ds.render_tiles(W, H, want_rgb=True)  # banded device-resident path (pinned to the restatement)
     big = np.full((H, W, 4), 5, dtype=np.uint8)
     reg = _abi.HostRegistration(big)
     try:
