@@ -156,7 +156,8 @@ enum : int {
     RGR_LOOP = 0, RGR_PRIM, RGR_PRIM_SPH_TAIL, RGR_PRIM_PLANE_DIV, RGR_GETCOLOR, RGR_NORMAL_SPHERE,
     RGR_BATCH, RGR_TEXEL, RGR_UV_SPHERE, RGR_UV_PLANE, RGR_LIGHT_SPH, RGR_REFRACT, RGR_SHADE, RGR_UNWIND,
     RGR_UNWIND_STEP, RGR_TILE_FETCH, RGR_Q_CLOSEST, RGR_Q_SHADOW, RGR_SH_GROUP, RGR_SH_TAIL, RGR_SH_PLANE,
-    RGR_SH_PLANE_DIV, RGR_QC_GROUP, RGR_QC_TAIL, RGR_QC_PLANE, RGR_PRIM_GROUP, RGR_PRIM_PLANE, RGR_DISK, RGR_BOX, RGR_COUNT
+    RGR_SH_PLANE_DIV, RGR_QC_GROUP, RGR_QC_TAIL, RGR_QC_PLANE, RGR_PRIM_GROUP, RGR_PRIM_PLANE, RGR_DISK, RGR_BOX,
+    RGR_PUSH_REFL, RGR_PUSH_REFR, RGR_UNWIND_REFRT, RGR_COUNT
 };
 #ifdef RG_REGION_STATS
 #define RG_REGION(k)                                                                                  \
@@ -1888,6 +1889,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             ret = cmul(cscl(col, m.transparency), surf);
                             unwind = true;
                         } else {
+                            RG_REGION(RGR_PUSH_REFR);  // frame writes: 18 dwords per lane (kr .. surf, pending ray, type)
                             auto &&f = stk[sp++];
                             f.f[0] = kr; f.f[1] = m.transparency;
                             f.f[2] = surf.r; f.f[3] = surf.g; f.f[4] = surf.b;
@@ -1971,6 +1973,7 @@ void rg_render_kernel(RgKernelArgs a) {
                         ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
                         unwind = true;
                     } else {
+                        RG_REGION(RGR_PUSH_REFL);  // frame writes: 5 dwords per lane (D.rgb, r, type)
                         auto &&f = stk[sp++];  // rendering.rs:88
                         f.type = FR_REFL;
                         f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = park[64 * PK_R];
@@ -2042,6 +2045,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             ret = cadd(cscl(dcol, 1.0f - r), cscl(def, r));
                             unwind = true;
                         } else {
+                            RG_REGION(RGR_PUSH_REFL);  // frame writes: 5 dwords per lane (D.rgb, r, type)
                             auto &&f = stk[sp++];
                             f.type = FR_REFL;
                             f.f[0] = dcol.r; f.f[1] = dcol.g; f.f[2] = dcol.b; f.f[3] = r;
@@ -2115,6 +2119,7 @@ void rg_render_kernel(RgKernelArgs a) {
                         ret = cadd(cscl(c3(f.f[0], f.f[1], f.f[2]), 1.0f - f.f[3]), cscl(ret, f.f[3]));
                         sp--;
                     } else if (f.type == FR_REFR_T) {
+                        RG_REGION(RGR_UNWIND_REFRT);  // frame writes: 4 dwords per lane (Tc.rgb, type)
                         f.f[5] = ret.r; f.f[6] = ret.g; f.f[7] = ret.b;
                         f.type = FR_REFR_R;
                         q.o = v3(f.rr[0], f.rr[1], f.rr[2]);

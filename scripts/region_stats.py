@@ -7,7 +7,7 @@ prints, per RG_REGION marker (rg_kernels.hip), how many times a wave entered the
 mean active lanes on entry.  scripts/isa_budget.py --visits multiplies these by each region's
 static instructions.
 
-    python scripts/region_stats.py [workload] [--json out.json]
+    python scripts/region_stats.py [workload] [--size WxH] [--json out.json]
 """
 import ctypes as C
 import json
@@ -32,21 +32,24 @@ def main():
 
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     out = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
-    if out in args:
-        args.remove(out)
+    size = sys.argv[sys.argv.index("--size") + 1] if "--size" in sys.argv else "3840x2160"
+    for v in (out, size):
+        if v in args:
+            args.remove(v)
+    W, H = (int(v) for v in size.split("x"))
     wl = args[0] if args else "test1"
-    scene, *_ = load_workload(wl, 3840, 2160)
+    scene, *_ = load_workload(wl, W, H)
     ds = DeviceScene(scene, device=0)
     st = _abi.rg_stats()
     ds.set_image_bands(1)
-    ds.render_tiles(3840, 2160, stats=st)
+    ds.render_tiles(W, H, stats=st)
     rn = names()
     w = (C.c_uint64 * (2 * len(rn)))()
     _abi.check(_abi.lib().rg_debug_counter_words(ds.handle, BASE, 2 * len(rn), w))
     ds.close()
     regs = {n: {"visits": int(w[2 * k]), "lanes_per_visit": round(int(w[2 * k + 1]) / max(int(w[2 * k]), 1), 2)}
             for k, n in enumerate(rn)}
-    res = {"workload": wl, "width": 3840, "height": 2160, "rays": st.rays.as_dict(), "regions": regs}
+    res = {"workload": wl, "width": W, "height": H, "rays": st.rays.as_dict(), "regions": regs}
     text = json.dumps(res, indent=1)
     if out:
         Path(out).write_text(text)
