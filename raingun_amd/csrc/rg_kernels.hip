@@ -78,7 +78,34 @@ __device__ __forceinline__ int32_t f32_to_i32(float v) {
     return (int32_t)v;
 }
 
+// Region visit counts (diagnostic build -DRG_REGION_STATS; scripts/region_stats.py): every time a
+// wave enters region k, its first active lane adds 1 to counters[RG_REGION_BASE + 2k] and the
+// active lanes to [+ 2k + 1] -- the dynamic weights of the static ISA budget (scripts/isa_budget.py).
+// Words 144.. lie in the lines of tile-queue heads 8-15, unused with RG_NQ = 8.
+#define RG_REGION_BASE 144
+enum : int {
+    RGR_LOOP = 0, RGR_PRIM, RGR_PRIM_SPH_TAIL, RGR_PRIM_PLANE_DIV, RGR_GETCOLOR, RGR_NORMAL_SPHERE,
+    RGR_BATCH, RGR_TEXEL, RGR_UV_SPHERE, RGR_UV_PLANE, RGR_LIGHT_SPH, RGR_REFRACT, RGR_SHADE, RGR_UNWIND,
+    RGR_UNWIND_STEP, RGR_TILE_FETCH, RGR_Q_CLOSEST, RGR_Q_SHADOW, RGR_SH_GROUP, RGR_SH_TAIL, RGR_SH_PLANE,
+    RGR_SH_PLANE_DIV, RGR_QC_GROUP, RGR_QC_TAIL, RGR_QC_PLANE, RGR_PRIM_GROUP, RGR_PRIM_PLANE, RGR_DISK, RGR_BOX,
+    RGR_PUSH_REFL, RGR_PUSH_REFR, RGR_UNWIND_REFRT, RGR_ERROR, RGR_SH_PAIR, RGR_PRIM_PAIR, RGR_QC_PAIR, RGR_COUNT
+};
+static_assert(RG_REGION_BASE + 2 * RGR_COUNT <= 16 + 16 * 15, "region counters stay below tile-queue head 15");
+#ifdef RG_REGION_STATS
+#define RG_REGION(k)                                                                                  \
+    do {                                                                                              \
+        const unsigned long long m_ = __ballot(1);                                                    \
+        if ((int)(threadIdx.x & 63u) == __builtin_ffsll((long long)m_) - 1) {                         \
+            atomicAdd(&a.counters[RG_REGION_BASE + 2 * (k)], 1ull);                                   \
+            atomicAdd(&a.counters[RG_REGION_BASE + 2 * (k) + 1], (unsigned long long)__builtin_popcountll(m_)); \
+        }                                                                                             \
+    } while (0)
+#else
+#define RG_REGION(k) do { } while (0)
+#endif
+
 __device__ __forceinline__ void raise_error(const RgKernelArgs &a, uint32_t pixel, int status) {
+    RG_REGION(RGR_ERROR);
     // lowest pixel wins: max of the complemented key; 0 (memset) = no error
     unsigned long long key = ((unsigned long long)pixel << 8) | (unsigned long long)(-status);
     atomicMax(&a.counters[3], ~key);
@@ -146,31 +173,6 @@ __device__ __forceinline__ bool disk_hit(const RgDsk &k, V3 o, V3 d, double &t) 
     t = dist;
     return true;
 }
-
-// Region visit counts (diagnostic build -DRG_REGION_STATS; scripts/region_stats.py): every time a
-// wave enters region k, its first active lane adds 1 to counters[RG_REGION_BASE + 2k] and the
-// active lanes to [+ 2k + 1] -- the dynamic weights of the static ISA budget (scripts/isa_budget.py).
-// Words 144.. lie in the lines of tile-queue heads 8-15, unused with RG_NQ = 8.
-#define RG_REGION_BASE 144
-enum : int {
-    RGR_LOOP = 0, RGR_PRIM, RGR_PRIM_SPH_TAIL, RGR_PRIM_PLANE_DIV, RGR_GETCOLOR, RGR_NORMAL_SPHERE,
-    RGR_BATCH, RGR_TEXEL, RGR_UV_SPHERE, RGR_UV_PLANE, RGR_LIGHT_SPH, RGR_REFRACT, RGR_SHADE, RGR_UNWIND,
-    RGR_UNWIND_STEP, RGR_TILE_FETCH, RGR_Q_CLOSEST, RGR_Q_SHADOW, RGR_SH_GROUP, RGR_SH_TAIL, RGR_SH_PLANE,
-    RGR_SH_PLANE_DIV, RGR_QC_GROUP, RGR_QC_TAIL, RGR_QC_PLANE, RGR_PRIM_GROUP, RGR_PRIM_PLANE, RGR_DISK, RGR_BOX,
-    RGR_PUSH_REFL, RGR_PUSH_REFR, RGR_UNWIND_REFRT, RGR_COUNT
-};
-#ifdef RG_REGION_STATS
-#define RG_REGION(k)                                                                                  \
-    do {                                                                                              \
-        const unsigned long long m_ = __ballot(1);                                                    \
-        if ((int)(threadIdx.x & 63u) == __builtin_ffsll((long long)m_) - 1) {                         \
-            atomicAdd(&a.counters[RG_REGION_BASE + 2 * (k)], 1ull);                                   \
-            atomicAdd(&a.counters[RG_REGION_BASE + 2 * (k) + 1], (unsigned long long)__builtin_popcountll(m_)); \
-        }                                                                                             \
-    } while (0)
-#else
-#define RG_REGION(k) do { } while (0)
-#endif
 
 // ---------------------------------------------------------------- sphere sources
 // The sphere tables are read with a wave-uniform index.  Three sources:
@@ -306,6 +308,9 @@ __device__ __forceinline__ void sph_primary_group(const RgKernelArgs &a, const S
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             double t;
+#ifdef RG_REGION_STATS
+            if (cand[k]) RG_REGION(RGR_PRIM_PAIR);
+#endif
             if (cand[k] && sphere_tail(s[k].r2, opp[k], adj[k], t)) closest_add(c, t, rg_cptr(a.sph_id)[i + k]);
         }
     }
@@ -378,6 +383,9 @@ __device__ __forceinline__ void sph_query_group(const RgKernelArgs &a, const Src
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             double t;
+#ifdef RG_REGION_STATS
+            if (cand[k]) RG_REGION(RGR_QC_PAIR);
+#endif
             if (cand[k] && sphere_tail(s[k].r2, opp[k], adj[k], t)) {
                 if (shadow) {
                     if (!(t > ld)) { occl = true; need = false; }
@@ -1009,6 +1017,9 @@ __device__ __forceinline__ void trace_shadow(const RgKernelArgs &a, const Src &s
 #pragma unroll
                 for (int l = 0; l < LB; ++l) {
                     double t;
+#ifdef RG_REGION_STATS
+                    if (k < g && cand[k][l]) RG_REGION(RGR_SH_PAIR);
+#endif
                     if (k < g && cand[k][l] && sphere_tail(s[k].r2, opp[k][l], adj[k][l], t) && !(t > sb.ld[l]))
                         occl |= 1u << l;
                 }

@@ -10,6 +10,17 @@ below (the sphere normal, the texel fetch, the spherical-light setup).  An instr
 the innermost region whose extent holds a frame of its chain.  Classes: FP64 (v_*_f64 and the
 division helpers), f32 VALU, int VALU, moves/selects, SALU, LDS, VMEM (global/scratch).
 
+Which binary: the -DRG_REGION_STATS build (--build stats, the default) -- the one whose visits are
+counted, so visits and static instructions describe the same code; the marker instrumentation
+itself (the instructions at RG_REGION lines) is left out.  The compiler unrolls loops, runtime ones
+too, so a marker can exist in several copies: a region's static figure is its instructions in one
+template instantiation over the marker copies that instantiation holds (each visit runs one copy).
+--build prod reads the production object instead (no marker copies to divide by: unrolled regions
+then show their copies' sum).  The sphere tails of the grouped miss tests (sphere_tail inlined into
+sph_primary_group / sph_query_group / trace_shadow) are regions of their own (RGR_*_PAIR, a visit
+per candidate (sphere, light) pair a wave runs), and raise_error is RGR_ERROR (no visits on a clean
+frame).
+
 Dynamic side (--visits region_stats.json from scripts/region_stats.py): each region's wave visits
 times its static instructions = the dynamic count; the sum is reconciled with the PMC counters
 (SQ_INSTS_VALU, the FP64 counters) of the same frame.
@@ -27,6 +38,9 @@ CSRC = Path(__file__).resolve().parent.parent / "raingun_amd" / "csrc"
 SRC = CSRC / "rg_kernels.hip"
 DEFAULT = "_Z16rg_render_kernelILi8ELb1ELb1ELi4ELi3ELb0ELb0ELb0ELi0ELb0EEv12RgKernelArgs"
 LLVM = "/opt/rocm/lib/llvm/bin"
+# callers of sphere_tail -> the pair region its inlined instructions belong to
+PAIR_OF = {"sph_primary_group": "RGR_PRIM_PAIR", "sph_query_group": "RGR_QC_PAIR", "trace_shadow": "RGR_SH_PAIR"}
+FUNCTION_REGIONS = {"RGR_NORMAL_SPHERE", "RGR_TEXEL", "RGR_UV_SPHERE", "RGR_UV_PLANE", "RGR_LIGHT_SPH"}
 CLASSES = ["fp64", "valu_f32", "valu_int", "move_select", "salu", "lds", "vmem"]
 VALU = CLASSES[:4]
 
@@ -166,11 +180,14 @@ def main():
             del args[k:k + 2]
             kernel, out_json, visits_path = ((v, out_json, visits_path) if flag == "--kernel" else
                                              (kernel, v, visits_path) if flag == "--json" else (kernel, out_json, v))
+    build = "stats"
+    if "--build" in args:
+        k = args.index("--build"); build = args[k + 1]; del args[k:k + 2]
     tmp = Path("/tmp/rg_isa_budget")
     tmp.mkdir(exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
            "-fPIC", "-gline-tables-only", "-DRG_DEV_LIGHT_ONLY", "-DRG_DEV_ONE_DEPTH", "-c", "rg_kernels.hip",
-           "-o", str(tmp / "k.o"), "--save-temps=obj", *args]
+           "-o", str(tmp / "k.o"), "--save-temps=obj", *(["-DRG_REGION_STATS"] if build == "stats" else []), *args]
     r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stderr[-3000:])
@@ -178,6 +195,10 @@ def main():
     obj = tmp / "rg_kernels-hip-amdgcn-amd-amdhsa-gfx950.out"
     regs = regions()
     names = region_names()
+    src_lines = SRC.read_text().splitlines()
+    marker_line = {i: m.group(1) for i, l in enumerate(src_lines, 1)
+                   for m in [re.search(r"RG_REGION\((RGR_\w+)\)", l)] if m and "#define" not in l}
+    markers = []  # (region, {full names on the chain}) per marker atomic
     per_inst = {}
     detail_lines = collections.defaultdict(collections.Counter)
     for sym, tag in ((kernel, None), ("_ZN3rgk9sphere_uvEdddd", "RGR_UV_SPHERE")):
@@ -185,6 +206,14 @@ def main():
         ch = chains(obj, [a for a, _ in insts])
         for (addr, op), chain in zip(insts, ch):
             reg, inst = tag, sym
+            mk = next(((fname, line) for _, fname, line, _ in chain if fname == "rg_kernels.hip"), None)
+            if build == "stats" and mk and mk[1] in marker_line:
+                if op.startswith("global_atomic_add"):
+                    markers.append((marker_line[mk[1]], {fr[3] for fr in chain}))
+                continue  # the instrumentation itself
+            tail = next((i for i, fr in enumerate(chain) if fr[0] == "sphere_tail"), None)
+            if reg is None and tail is not None and tail + 1 < len(chain) and chain[tail + 1][0] in PAIR_OF:
+                reg, inst = PAIR_OF[chain[tail + 1][0]], chain[tail + 1][3]
             if reg is None:
                 best = None
                 for depth, (f, fname, line, full) in enumerate(chain):  # innermost first
@@ -197,13 +226,28 @@ def main():
                     if best is not None:
                         break
                 reg, inst = (best[1], best[2]) if best else ("(outside the loop)", sym)
+                if reg in FUNCTION_REGIONS:
+                    inst = "(all)"  # spans several functions (light_dir_dist + light_intensity): one sum
             # per template instantiation of the region's function (sph_query_group<2> and its
             # remainder copy <1> hold the same lines): the largest one is what a visit runs
             per_inst.setdefault(reg, {}).setdefault(inst, collections.Counter())[klass(op)] += 1
             if detail and reg == detail:
                 key = " < ".join(f"{f}:{line}" for f, _, line, _ in chain[:4])
                 detail_lines[key][klass(op)] += 1
-    static = {reg: max(d.values(), key=lambda c: sum(c[k] for k in VALU)) for reg, d in per_inst.items()}
+    def copies(reg, inst):
+        """Marker copies (atomic pairs) of reg inside instantiation inst, else in the whole kernel."""
+        mine = [f for r, f in markers if r == reg]
+        n = sum(1 for f in mine if inst in f) or len(mine)
+        return max(1, n // 2)
+    static, ncopies = {}, {}
+    for reg, d in per_inst.items():
+        inst, c = max(d.items(), key=lambda kv: sum(kv[1][k] for k in VALU))
+        n = copies(reg, inst) if build == "stats" else 1
+        ncopies[reg] = n
+        static[reg] = collections.Counter({k: round(v / n) for k, v in c.items()})
+    if build == "stats":
+        print("marker copies per visited instantiation: " +
+              ", ".join(f"{k[4:]}={v}" for k, v in sorted(ncopies.items()) if v > 1))
     visits = None
     if visits_path:
         visits = json.loads(Path(visits_path).read_text())["regions"]

@@ -7,7 +7,7 @@ prints, per RG_REGION marker (rg_kernels.hip), how many times a wave entered the
 mean active lanes on entry.  scripts/isa_budget.py --visits multiplies these by each region's
 static instructions.
 
-    python scripts/region_stats.py [workload] [--size WxH] [--json out.json]
+    python scripts/region_stats.py [workload] [--size WxH] [--json out.json] [--lib abvar/region/libraingun_hip.so]
 """
 import ctypes as C
 import json
@@ -26,6 +26,11 @@ def names():
 
 
 def main():
+    if "--lib" in sys.argv:  # the RG_REGION_STATS build (before _abi loads the default library)
+        import os
+        k = sys.argv.index("--lib")
+        os.environ["RAINGUN_HIP_LIB"] = str(Path(sys.argv[k + 1]).resolve())
+        del sys.argv[k:k + 2]
     from bench import load_workload
     from raingun_amd import _abi
     from raingun_amd.scene import DeviceScene
