@@ -88,7 +88,8 @@ enum : int {
     RGR_BATCH, RGR_TEXEL, RGR_UV_SPHERE, RGR_UV_PLANE, RGR_LIGHT_SPH, RGR_REFRACT, RGR_SHADE, RGR_UNWIND,
     RGR_UNWIND_STEP, RGR_TILE_FETCH, RGR_Q_CLOSEST, RGR_Q_SHADOW, RGR_SH_GROUP, RGR_SH_TAIL, RGR_SH_PLANE,
     RGR_SH_PLANE_DIV, RGR_QC_GROUP, RGR_QC_TAIL, RGR_QC_PLANE, RGR_PRIM_GROUP, RGR_PRIM_PLANE, RGR_DISK, RGR_BOX,
-    RGR_PUSH_REFL, RGR_PUSH_REFR, RGR_UNWIND_REFRT, RGR_ERROR, RGR_SH_PAIR, RGR_PRIM_PAIR, RGR_QC_PAIR, RGR_COUNT
+    RGR_PUSH_REFL, RGR_PUSH_REFR, RGR_UNWIND_REFRT, RGR_ERROR, RGR_SH_PAIR, RGR_PRIM_PAIR, RGR_QC_PAIR,
+    RGR_WALK, RGR_WALK_LEAF, RGR_LB_SHADOW, RGR_COUNT
 };
 static_assert(RG_REGION_BASE + 2 * RGR_COUNT <= 16 + 16 * 15, "region counters stay below tile-queue head 15");
 #ifdef RG_REGION_STATS
@@ -672,6 +673,7 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
         }
 #endif
         if (act) {
+            RG_REGION(RGR_WALK);  // per-lane walk iteration (heavy path)
             // the node's children without divergent branches: every slot's slab test,
             // hit leaves as a bit mask (tested below in child order), hit internal
             // children as sort keys (~0: none), pushes written unconditionally
@@ -688,6 +690,7 @@ __device__ __forceinline__ void bvh_lane(const RgKernelArgs &a, const Src &src, 
             }
             // leaves first (they tighten a closest-hit bound), in child order
             while (leaves != 0u && need) {
+                RG_REGION(RGR_WALK_LEAF);
                 const uint32_t k = (uint32_t)__builtin_ctz(leaves);
                 leaves &= leaves - 1u;
                 const int v = ~(k == 0u ? N.child[0] : k == 1u ? N.child[1] : k == 2u ? N.child[2] : N.child[3]);
@@ -759,6 +762,7 @@ template <class Src>
 __device__ __forceinline__ void lbuf_shadow(const RgKernelArgs &a, const Src &src, int light, const LbRange &r, V3 o,
                                             V3 d, double ld, bool &occl, bool &need) {
     const RgLightBufDev &B = src.lb[light];
+    RG_REGION(RGR_LB_SHADOW);
     const RayF rf = make_rayf(o, d);
     Closest unused;
     closest_init(unused);
