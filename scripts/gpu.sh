@@ -27,7 +27,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 export TMPDIR=/tmp
 log() { echo "[$(date +%H:%M:%S)] $*" | tee -a "$O/session.txt"; }
-sp() { local x="${1//,/ }"; x="${x//@/::}"; echo "${x//\~/:}"; }  # "," -> " ", "@" -> "::" (pytest node ids), "~" -> ":"
+sp() { local x="${1//,/ }"; x="${x//@/::}"; x="${x//^/,}"; echo "${x//\~/:}"; }  # "," -> " ", "@" -> "::" (pytest node ids), "^" -> ",", "~" -> ":"
 
 for step in "$@"; do
   IFS=':' read -r kind a1 a2 a3 a4 <<< "$step"
