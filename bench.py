@@ -527,6 +527,9 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
     return res
 
 
+HV_INSTANCES = 3  # scene instances the pinned host-visible frame is timed on (median reported)
+
+
 def host_visible(workload: str, args, dev, W: int = 3840, H: int = 2160, budget_s: float = 2.0):
     """The drop-in itself: rg_render_image (rendering.rs:24-38) returns the frame
     in HOST memory.  Timed back to back into a page-locked buffer
@@ -547,25 +550,47 @@ def host_visible(workload: str, args, dev, W: int = 3840, H: int = 2160, budget_
     ref = ds.render_image(W, H, stats=st)
     rays = st.rays.primary + st.rays.shadow + st.rays.secondary
     res = {"workload": label, "basis": "rg_render_image back to back: frame in host memory when each call returns "
-                                       "(PCIe included; scene already in HBM)"}
-    for kind in ("pinned", "pageable"):
-        buf = np.empty((H, W, 4), dtype=np.uint8)
-        reg = _abi.HostRegistration(buf) if kind == "pinned" else None
-        try:
-            for _ in range(3):
-                ds.render_image(W, H, out=buf)
-            n, t0 = 0, time.perf_counter()
-            while n < 5 or (time.perf_counter() - t0 < budget_s and n < args.steps):
-                ds.render_image(W, H, out=buf)
-                n += 1
-            dt = (time.perf_counter() - t0) / n
-            if not np.array_equal(buf, ref):
-                raise SystemExit("host_visible: frame differs from the first render")
-        finally:
-            if reg is not None:
-                reg.close()
-        res[kind] = {"value": round(rays / dt / 1e6, 3), "ms_per_step": round(dt * 1e3, 4), "frames": n,
-                     "frame_bytes": H * W * 4, "host_GBps": round(H * W * 4 / dt / 1e9, 2)}
+                                       "(PCIe included; scene already in HBM); pinned: the median of "
+                                       f"{HV_INSTANCES} scene instances"}
+
+    def frames(d, buf, budget):
+        for _ in range(3):
+            d.render_image(W, H, out=buf)
+        n, t0 = 0, time.perf_counter()
+        while n < 5 or (time.perf_counter() - t0 < budget and n < args.steps):
+            d.render_image(W, H, out=buf)
+            n += 1
+        dt = (time.perf_counter() - t0) / n
+        if not np.array_equal(buf, ref):
+            raise SystemExit("host_visible: frame differs from the first render")
+        return dt, n
+
+    def line(dt, n):
+        return {"value": round(rays / dt / 1e6, 3), "ms_per_step": round(dt * 1e3, 4), "frames": n,
+                "frame_bytes": H * W * 4, "host_GBps": round(H * W * 4 / dt / 1e9, 2)}
+
+    # Pinned: one DeviceScene instance can run its host frame ~12 % slower than another of the same
+    # scene in the same process -- 1 instance in 4 on the north star, the same instance every time
+    # it is timed, with its device-resident launch unchanged (profiles/r06/s20-s22; most likely the
+    # hardware queue its streams land on) -- so the frame is timed on HV_INSTANCES instances
+    buf = np.empty((H, W, 4), dtype=np.uint8)
+    reg = _abi.HostRegistration(buf)
+    inst = []
+    try:
+        for i in range(HV_INSTANCES):
+            d = ds if i == 0 else DeviceScene(scene, device=dev.index or 0)
+            try:
+                inst.append(frames(d, buf, budget_s / HV_INSTANCES))
+            finally:
+                if d is not ds:
+                    d.close()
+    finally:
+        reg.close()
+    med = sorted(inst)[len(inst) // 2]
+    res["pinned"] = line(*med)
+    res["pinned"]["instances_ms"] = [round(dt * 1e3, 4) for dt, _ in inst]
+    buf = np.empty((H, W, 4), dtype=np.uint8)
+    res["pageable"] = line(*frames(ds, buf, budget_s))
     res["multi_8gpu_rehearsal"] = multi_rehearsal(ds, W, H, res["pinned"]["ms_per_step"], args, split=True)
     ds.close()
     torch.cuda.synchronize(dev)
@@ -662,7 +687,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def main() -> None:
+def parse_args(argv=None) -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs of this node (one process each).  Outside a launcher, N > 1 starts "
@@ -716,7 +741,11 @@ def main() -> None:
                          "with --rccl-rehearsal; this flag adds it at N = 1)")
     ap.add_argument("--plan", action="store_true",
                     help="print this rank's launch plan (rank, world, device) as JSON and exit before any GPU work")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main() -> None:
+    args = parse_args()
 
     # One process per GPU.  `--gpus N` outside a launcher: start torch.distributed.run
     # with N ranks on this node as a CHILD process (nothing here has touched the GPU
