@@ -247,6 +247,9 @@ __host__ __device__ inline unsigned long long rg_tile_count(const RgKernelArgs &
 #ifndef RG_LB
 #define RG_LB 3                   // lights per shadow batch on the light path (its LB template parameter)
 #endif
+#ifndef RG_LB_SMALL
+#define RG_LB_SMALL 2             // light scenes with at most this many lights run a batch this wide (0: off)
+#endif
 #ifndef RG_HEAVY_WPS
 #define RG_HEAVY_WPS 3            // heavy path: waves per SIMD (block = 256 * WPS threads; 168 VGPRs)
 #endif

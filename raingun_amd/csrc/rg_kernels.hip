@@ -283,7 +283,9 @@ __device__ __forceinline__ bool filter_primary(const RgSphF &f, const RgSphF2 &f
     return !(opp > f2.thrp);
 }
 
+#ifndef RG_SPH_GROUP
 #define RG_SPH_GROUP 2     // spheres per exact miss-test group (one divergent branch per group)
+#endif
 #define RG_FILTER_GROUP 4  // spheres per f32-filter group (2 and 8 measured slower)
 
 // Primary rays start at the origin (ray.rs:53): h = c - 0 = c exactly, so
@@ -2894,14 +2896,24 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
             // VGPRs) measured slower into pinned memory, 0.768 -> 0.826 ms (profiles/r06/s5)
             return hipErrorInvalidValue;
         } else {
-            if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT) {
-                // a launch on its own (not one of several frames in flight): persistent waves at full
-                // occupancy balance the tiles dynamically, where a fixed tiles-per-wave grid makes every
-                // wave render exactly that many tiles and the slowest wave's sum the makespan
-                // (2: launches below RG_LIGHT_BIG_TILES tiles only -- rg_render_multi's shares and bands)
-                if (!a->pipelined && (RG_LIGHT_SINGLE_PERSISTENT != 2 || rg_tile_count(*a) < RG_LIGHT_BIG_TILES))
-                    return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, -1>(a, stream, gt);
+            // a launch on its own (not one of several frames in flight): persistent waves at full
+            // occupancy balance the tiles dynamically, where a fixed tiles-per-wave grid makes every
+            // wave render exactly that many tiles and the slowest wave's sum the makespan
+            // (2: launches below RG_LIGHT_BIG_TILES tiles only -- rg_render_multi's shares and bands)
+            const bool persistent = MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT && !a->pipelined &&
+                                    (RG_LIGHT_SINGLE_PERSISTENT != 2 || rg_tile_count(*a) < RG_LIGHT_BIG_TILES);
+#if RG_LB_SMALL > 1
+            // scenes with at most RG_LB_SMALL lights: a batch that wide, not RG_LB (the per-light
+            // loops of the shadow batch are unrolled over LB; test3's one light: 0.2525 -> 0.2293 ms
+            // at LB 2, profiles/r06/s24)
+            if (a->n_lights <= RG_LB_SMALL) {
+                if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT)
+                    if (persistent) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB_SMALL, false, false, false, -1>(a, stream, gt);
+                return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB_SMALL, false, false, false>(a, stream, gt);
             }
+#endif
+            if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT)
+                if (persistent) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, -1>(a, stream, gt);
             return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false>(a, stream, gt);
         }
     }

@@ -101,6 +101,16 @@ def test_synthetic(oracle_lib, n, planes, depth, w, h, path, bvh, lane):
     _compare(oracle_lib, synthetic_scene(n, planes, depth), w, h, path=path, bvh=bvh, lane=lane)
 
 
+@pytest.mark.parametrize("keep", [[0], [1], [0, 1], [1, 2], [0, 1, 2]])
+@pytest.mark.parametrize("path", PATHS)
+def test_light_counts(oracle_lib, example_scenes, keep, path):
+    """test1 with 1, 2 or 3 of its lights: the light path runs a 2-light shadow batch for scenes
+    with at most RG_LB_SMALL (2) lights and the 3-light one otherwise (rg_kernels.hip launch_depth)."""
+    scene = copy.deepcopy(example_scenes["test1"])
+    scene.lights = [scene.lights[i] for i in keep]
+    _compare(oracle_lib, scene, 320, 240, path=path)
+
+
 @pytest.mark.parametrize("n,planes,depth,w,h", [(16, 2, 5, 320, 240), (1024, 2, 5, 192, 108), (40, 4, 20, 160, 90)])
 @pytest.mark.parametrize("lane", [None, 0])
 def test_synthetic_shadow_rays_walk_the_bvh(oracle_lib, n, planes, depth, w, h, lane):
