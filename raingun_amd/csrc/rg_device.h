@@ -250,6 +250,9 @@ __host__ __device__ inline unsigned long long rg_tile_count(const RgKernelArgs &
 #ifndef RG_LB_SMALL
 #define RG_LB_SMALL 2             // light scenes with at most this many lights run a batch this wide (0: off)
 #endif
+#ifndef RG_LB_ONE
+#define RG_LB_ONE 1               // light scenes with one light (or none) run a batch of one
+#endif
 #ifndef RG_HEAVY_WPS
 #define RG_HEAVY_WPS 3            // heavy path: waves per SIMD (block = 256 * WPS threads; 168 VGPRs)
 #endif

@@ -1569,14 +1569,17 @@ __device__ __forceinline__ void stage16(unsigned char *dst, const void *src, uin
 // walk stacks -- scenes whose sphere tables exceed the budget), then every wave repeatedly takes the next 8x8 pixel
 // tile from an atomic queue (counters[16..], sharded) and runs the per-lane
 // state machine until its 64 lanes have written their pixels.
-template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 0,
+template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LBT, bool F32F, bool BVH, bool TASKS, int TPW = 0,
           bool HF = false>
+// LBT: lights per shadow batch on the light path (2, 3; -1: one light), 1: the heavy path.
 // HF: the host-frame features (HOSTF below) with MAXD array frames.  TPW: light path, tiles per wave (0: RG_LIGHT_TILES_PER_WAVE; < 0: persistent waves that take tiles
 // until the queue is empty -- single launches, whose makespan is their slowest wave's tile sum).  Light path (LB > 1): blocks of RG_LIGHT_BLOCK_WAVES waves, at least WPS waves
 // per SIMD (the second bound is waves per execution unit on AMD); heavy path:
 // one block of 4*WPS waves per CU.  Both cap the VGPRs at 512 / WPS.
-__global__ __launch_bounds__(LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS, LB > 1 ? WPS : 1)
+__global__ __launch_bounds__(LBT != 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS, LBT != 1 ? WPS : 1)
 void rg_render_kernel(RgKernelArgs a) {
+    constexpr int LB = LBT < 0 ? -LBT : LBT;  // lights per shadow batch (1 on the heavy path)
+    constexpr bool LIGHTP = LBT != 1;         // the light path
     static_assert(!BVH || 4 * WPS <= RG_BVH_MAX_WAVES, "one BVH stack per wave");
 #ifdef RG_WAVE_TIMES  // diagnostic: per-wave start (before staging), staged, end (100 MHz ticks), tiles
     const unsigned long long t_wave0 = wall_clock64();
@@ -1593,7 +1596,7 @@ void rg_render_kernel(RgKernelArgs a) {
     Cold T;
     // light path: every one-wave block stages its own copy of the (few-KB) scene; with the
     // arena's device image that is one loop with all its loads in flight at once
-    const bool blob = LB > 1 && LSPH && LCOLD && a.lds_blob != nullptr;
+    const bool blob = LIGHTP && LSPH && LCOLD && a.lds_blob != nullptr;
     if (blob) {
         const uint4 *g = reinterpret_cast<const uint4 *>(a.lds_blob);
         uint4 *d = reinterpret_cast<uint4 *>(smem);
@@ -1688,7 +1691,7 @@ void rg_render_kernel(RgKernelArgs a) {
     // instantiations of device-resident renders stay as lean as before (the
     // runtime checks alone cost test1 3 %, profiles/r02/ab_hostf.txt).
     constexpr bool HOSTF = MAXD == 0 || HF;
-    __shared__ uint32_t tile_px[HOSTF ? (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) : 1][64];
+    __shared__ uint32_t tile_px[HOSTF ? (LIGHTP ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) : 1][64];
     uint32_t *my_px = &tile_px[HOSTF ? threadIdx.x >> 6 : 0][lane];
     // Light path into page-locked host memory without tile publication: the
     // finished tiles of a wave collect in an LDS ring and go out RING at a time.
@@ -1696,7 +1699,7 @@ void rg_render_kernel(RgKernelArgs a) {
     // gfx9 every later `s_waitcnt vmcnt` (a texel load, a frame pop from the
     // global frame buffer) waits for it too: one flush per RING tiles instead of
     // one per tile.
-    constexpr int RING = (HOSTF && LB > 1) ? RG_HOST_RING : 0;
+    constexpr int RING = (HOSTF && LIGHTP) ? RG_HOST_RING : 0;
     __shared__ uint32_t ring_px[RING > 0 ? RG_LIGHT_BLOCK_WAVES : 1][RING > 0 ? RING : 1][64];
     __shared__ uint32_t ring_tile[RING > 0 ? RG_LIGHT_BLOCK_WAVES : 1][RING > 0 ? RING : 1];
     [[maybe_unused]] const uint32_t rw = RING > 0 ? (threadIdx.x >> 6) % RG_LIGHT_BLOCK_WAVES : 0u;
@@ -1707,8 +1710,8 @@ void rg_render_kernel(RgKernelArgs a) {
     // that only the query's own state is held in VGPRs across the trace.
     constexpr int PK_PP = 0, PK_LIN = LB, PK_REFL = 2 * LB, PK_COL = 2 * LB + 1, PK_KIND = 2 * LB + 4,
                   PK_R = 2 * LB + 5, PK_N = 2 * LB + 6;
-    __shared__ float park_lds[LB > 1 ? RG_LIGHT_BLOCK_WAVES : 1][LB > 1 ? PK_N : 1][64];
-    float *park = &park_lds[LB > 1 ? (threadIdx.x >> 6) % RG_LIGHT_BLOCK_WAVES : 0][0][lane];  // field k at park[64 k]
+    __shared__ float park_lds[LIGHTP ? RG_LIGHT_BLOCK_WAVES : 1][LIGHTP ? PK_N : 1][64];
+    float *park = &park_lds[LIGHTP ? (threadIdx.x >> 6) % RG_LIGHT_BLOCK_WAVES : 0][0][lane];  // field k at park[64 k]
 #ifdef RG_BVH_STATS
     if (lane < 16) rg_stat_lds[(threadIdx.x >> 6) % RG_BVH_MAX_WAVES][lane] = 0ull;
 #endif
@@ -1791,7 +1794,7 @@ void rg_render_kernel(RgKernelArgs a) {
 #endif
     for (;;) {
         RG_REGION(RGR_LOOP);
-        if constexpr (LB == 1 && TASKS && RG_SHADOW_FAN > 0) {
+        if constexpr (!LIGHTP && TASKS && RG_SHADOW_FAN > 0) {
             // shadow fan-out, collect: the helpers' occlusion bits (every lane active here)
             if (__any(nfan > 0)) {
                 fan_bits = 0u;
@@ -1827,7 +1830,7 @@ void rg_render_kernel(RgKernelArgs a) {
                     V3 n;
                     if (!surface_normal(b, h, n)) raise_error(a, pixel, RG_ERR_AABB_NORMAL);
                     if (m.surface != RG_SURFACE_REFRACTIVE) {
-                        if constexpr (LB > 1) {
+                        if constexpr (LIGHTP) {
                             // ONE batch covers every light (n_lights <= LB on this path): set it
                             // up now, with the per-light shading factors (parked in LDS), so that
                             // no hit-point state (h, n, incident) has to survive the shadow pass
@@ -1962,7 +1965,7 @@ void rg_render_kernel(RgKernelArgs a) {
             } else if (rmode == MODE_SHADOW) {
                 shade = true;  // a shadow result for light li
             }
-            if constexpr (LB > 1) {
+            if constexpr (LIGHTP) {
               if (shade) {
                 RG_REGION(RGR_SHADE);
                 // shade_diffuse accumulation over the batch (rendering.rs:141-170), in light order
@@ -2018,7 +2021,7 @@ void rg_render_kernel(RgKernelArgs a) {
                             fin = cadd(fin, cmul(bcol, lc));
                         }
                     }
-                    if constexpr (LB == 1 && TASKS && RG_SHADOW_FAN > 0) {
+                    if constexpr (!LIGHTP && TASKS && RG_SHADOW_FAN > 0) {
                         // the lights helper lanes traced, in light order (rendering.rs:141-170)
                         for (int k = 0; k < nfan; ++k) {
                             const RgLightDev L = T.lights[li + 1 + k];
@@ -2201,7 +2204,7 @@ void rg_render_kernel(RgKernelArgs a) {
             // nor in the light path's persistent single launches (TPW < 0), for the same reason:
             // rg_render_multi's shares, whose waves ended by 84 us (p50) while claimed tiles still
             // started at 145 us (profiles/r05/s18, s26)
-            if constexpr (!HOSTF && LB > 1 && TPW >= 0) {
+            if constexpr (!HOSTF && LIGHTP && TPW >= 0) {
                 if (pf_valid) {  // the slot claimed at the previous tile's start
                     const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)pf_k, 0, 64));
                     const unsigned long long t = (unsigned long long)k * RG_NQ + qi;
@@ -2236,14 +2239,14 @@ void rg_render_kernel(RgKernelArgs a) {
                 tiles_left = false;
             } else {
                 constexpr uint32_t kmax = MAXD == 0 || HF || TPW < 0 ? 0u
-                                          : LB > 1 ? (TPW > 0 ? (uint32_t)TPW : RG_LIGHT_TILES_PER_WAVE)
+                                          : LIGHTP ? (TPW > 0 ? (uint32_t)TPW : RG_LIGHT_TILES_PER_WAVE)
                                                    : RG_HEAVY_TILES_PER_WAVE;
                 if constexpr (kmax > 0) {
                     // non-persistent: a wave renders at most kmax tiles, so the grid
                     // drains through the hardware dispatcher wave (block) by wave
                     if (++tiles_taken >= kmax) tiles_left = false;
                 }
-                if constexpr (!HOSTF && LB > 1 && TPW >= 0) {
+                if constexpr (!HOSTF && LIGHTP && TPW >= 0) {
                     // claim the wave's NEXT queue slot now: the atomic's round trip overlaps this
                     // tile's work instead of stalling the wave between tiles (the wave renders
                     // the claimed tile, or finds the head drained, at its next tile start)
@@ -2288,7 +2291,7 @@ void rg_render_kernel(RgKernelArgs a) {
                     // heavy path: the host's per-column / per-row table of the same expressions
                     // (north star -1 %); the light path keeps the divisions (the loads at the
                     // tile's start cost it more than they save: test1 +0.5 %, test3 +1.5 %)
-                    if (LB == 1 && a.prim_sx) {
+                    if (!LIGHTP && a.prim_sx) {
                         sx = a.prim_sx[x];
                         sy = a.prim_sy[y];
                     } else {
@@ -2308,7 +2311,7 @@ void rg_render_kernel(RgKernelArgs a) {
                 continue;
             }
         }
-        if constexpr (LB == 1 && TASKS && RG_SHADOW_FAN > 0) {
+        if constexpr (!LIGHTP && TASKS && RG_SHADOW_FAN > 0) {
             // shadow fan-out, assign: a lane about to trace the shadow ray of light li
             // hands lights li+1.. of the same hit to idle lanes of its wave, so up to
             // 1 + RG_SHADOW_FAN shadow rays of a hit are traced in one iteration instead
@@ -2418,7 +2421,7 @@ void rg_render_kernel(RgKernelArgs a) {
                     atomicAdd(&a.counters[11], (unsigned long long)__builtin_popcountll(shl));
                 }
                 // light path (no BVH walk words): iterations with closest-hit lanes, those lanes
-                if (LB > 1 && (all & ~shl)) {
+                if (LIGHTP && (all & ~shl)) {
                     atomicAdd(&a.counters[14], 1ull);
                     atomicAdd(&a.counters[15], (unsigned long long)__builtin_popcountll(all & ~shl));
                 }
@@ -2433,7 +2436,7 @@ void rg_render_kernel(RgKernelArgs a) {
             closest_init(c);
             occl = 0u;
         }
-        if constexpr (LB == 1) {
+        if constexpr (!LIGHTP) {
             // one ray per lane, one pass: closest-hit and shadow lanes share the
             // body loop (best when a wave mixes ray kinds over many bodies)
             if (querying) {
@@ -2800,16 +2803,16 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
     // and with frames in flight the next frame's blocks take the slots of
     // waves that finished (a 4*WPS-wave block would keep the CU until its
     // slowest wave -- one refractive tile -- is done).
-    constexpr int threads = LB > 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS;  // LB > 1: the light path
+    constexpr int threads = LB != 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS;  // LB != 1: the light path
     auto kern = rg_render_kernel<MAXD, LSPH, LCOLD, WPS, LB, F32F, BVH, TASKS, TPW, HF>;
     int cus = 0, per_cu = 0;
     const hipError_t oe = occupancy(reinterpret_cast<const void *>(kern), threads, lds, cus, per_cu);
     if (oe != hipSuccess) return oe;
-    if ((MAXD == 0 || HF) && LB > 1 && per_cu > RG_DEEP_BLOCKS_PER_CU) per_cu = RG_DEEP_BLOCKS_PER_CU;
+    if ((MAXD == 0 || HF) && LB != 1 && per_cu > RG_DEEP_BLOCKS_PER_CU) per_cu = RG_DEEP_BLOCKS_PER_CU;
     // light single launches, persistent waves (TPW < 0): RG_LIGHT_PERSIST_BLOCKS_PER_CU one-wave
     // blocks per CU (2 per SIMD), never more than the occupancy query admits (a scene whose LDS
     // copy allows fewer would otherwise start the extra blocks only after the queue drained)
-    if (MAXD != 0 && LB > 1 && TPW < 0) per_cu = std::min(per_cu, RG_LIGHT_PERSIST_BLOCKS_PER_CU);
+    if (MAXD != 0 && LB != 1 && TPW < 0) per_cu = std::min(per_cu, RG_LIGHT_PERSIST_BLOCKS_PER_CU);
     const unsigned long long tiles = rg_tile_count(*a);
     const unsigned long long waves = (unsigned long long)threads / 64u;
     unsigned long long blocks = (unsigned long long)cus * per_cu;
@@ -2827,7 +2830,7 @@ static hipError_t launch_one(const RgKernelArgs *a, size_t lds, hipStream_t stre
         if (cap < floor_blocks) cap = floor_blocks;
         if (blocks > cap) blocks = cap;
     }
-    constexpr unsigned long long kmax = MAXD == 0 || HF || TPW < 0 ? 0 : LB > 1 ? (TPW > 0 ? TPW : RG_LIGHT_TILES_PER_WAVE) : RG_HEAVY_TILES_PER_WAVE;
+    constexpr unsigned long long kmax = MAXD == 0 || HF || TPW < 0 ? 0 : LB != 1 ? (TPW > 0 ? TPW : RG_LIGHT_TILES_PER_WAVE) : RG_HEAVY_TILES_PER_WAVE;
     if constexpr (kmax > 0)  // non-persistent: one wave per kmax tiles
         blocks = (tiles + waves * kmax - 1) / (waves * kmax);
     if (a->max_grid_threads && blocks * threads > a->max_grid_threads) blocks = a->max_grid_threads / threads;
@@ -2854,7 +2857,7 @@ template <int MAXD, int WPS, int LB, bool F32F, bool BVH, bool TASKS, int TPW = 
 static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t *gt) {
     // the BVH kernels also hold the static per-wave traversal stacks
     constexpr uint32_t budget = RG_LDS_BUDGET - (BVH ? (uint32_t)sizeof(rg_bvh_stack) : 0u) -
-                                (uint32_t)(MAXD != 0 && !HF ? 0 : (LB > 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) * 64 * 4) -  // tile_px
+                                (uint32_t)(MAXD != 0 && !HF ? 0 : (LB != 1 ? RG_LIGHT_BLOCK_WAVES : 4 * WPS) * 64 * 4) -  // tile_px
                                 (TASKS ? (uint32_t)sizeof(TaskPool) : 0u);
     if (a->lds_total_bytes <= budget)  // whole scene (empty sphere part if n_sph == 0)
         return launch_one<MAXD, true, true, WPS, LB, F32F, BVH, TASKS, TPW, HF>(a, a->lds_total_bytes, stream, gt);
@@ -2902,6 +2905,14 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
             // (2: launches below RG_LIGHT_BIG_TILES tiles only -- rg_render_multi's shares and bands)
             const bool persistent = MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT && !a->pipelined &&
                                     (RG_LIGHT_SINGLE_PERSISTENT != 2 || rg_tile_count(*a) < RG_LIGHT_BIG_TILES);
+#if RG_LB_ONE
+            // one-light scenes: a batch of one (template LBT -1: 1 is the heavy path)
+            if (a->n_lights <= 1) {
+                if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT)
+                    if (persistent) return launch_waves<MAXD, RG_LIGHT_WPS, -1, false, false, false, -1>(a, stream, gt);
+                return launch_waves<MAXD, RG_LIGHT_WPS, -1, false, false, false>(a, stream, gt);
+            }
+#endif
 #if RG_LB_SMALL > 1
             // scenes with at most RG_LB_SMALL lights: a batch that wide, not RG_LB (the per-light
             // loops of the shadow batch are unrolled over LB; test3's one light: 0.2525 -> 0.2293 ms
