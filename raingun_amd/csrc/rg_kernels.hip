@@ -2884,6 +2884,9 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 #ifndef RG_LIGHT_WPS
 #define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
 #endif
+#ifndef RG_LIGHT_WPS_ONE
+#define RG_LIGHT_WPS_ONE RG_LIGHT_WPS  // the one-light batch (118 VGPRs at 4 waves per SIMD)
+#endif
 
 template <int MAXD, bool HF = false>
 static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t *gt) {
@@ -2909,8 +2912,8 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
             // one-light scenes: a batch of one (template LBT -1: 1 is the heavy path)
             if (a->n_lights <= 1) {
                 if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT)
-                    if (persistent) return launch_waves<MAXD, RG_LIGHT_WPS, -1, false, false, false, -1>(a, stream, gt);
-                return launch_waves<MAXD, RG_LIGHT_WPS, -1, false, false, false>(a, stream, gt);
+                    if (persistent) return launch_waves<MAXD, RG_LIGHT_WPS_ONE, -1, false, false, false, -1>(a, stream, gt);
+                return launch_waves<MAXD, RG_LIGHT_WPS_ONE, -1, false, false, false>(a, stream, gt);
             }
 #endif
 #if RG_LB_SMALL > 1
