@@ -243,6 +243,22 @@ def gather_rank_times(elapsed_s: float, steps: int, kernel_ms: float, world: int
     return sorted(out, key=lambda r: r["rank"])
 
 
+_RENDER_STREAMS = {}
+
+
+def render_streams(dev, n: int):
+    """The render streams of the frames in flight, made once per process and reused by every line.
+    HIP maps each new stream to the next hardware queue; a line timed on streams made later in the
+    process landed on other queues and ran slower: test3 0.219 ms as the first line, 0.243 ms after
+    test1 on new streams (profiles/r06/s29, s30)."""
+    import torch
+
+    key = (dev.index or 0, n)
+    if key not in _RENDER_STREAMS:
+        _RENDER_STREAMS[key] = [torch.cuda.Stream(dev) for _ in range(n)]
+    return _RENDER_STREAMS[key]
+
+
 def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cpu: bool, size=None,
             steps=None, warmup=None, budget_s=None):
     """Time `steps` frames of `workload` on this rank (after `warmup`), frame
@@ -346,7 +362,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
                 "communicator": "ncclCommInitRank (rg_comm_init_rank; unique id broadcast by torch.distributed)"}
     if not native and use_pipe:
         pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TR, device=dev, depth=F,
-                                streams=F > 1 and not args.one_render_stream, gather=gather)
+                                streams=render_streams(dev, F) if F > 1 and not args.one_render_stream else False,
+                                gather=gather)
 
     def step():
         if native:

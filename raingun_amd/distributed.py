@@ -227,7 +227,7 @@ class FramePipeline:
     stream, so the two launches never share counters or tile queues."""
 
     def __init__(self, part_shape, height: int, rank: int, world: int, tile_rows: int = TILE_ROWS,
-                 device=None, depth: int = 2, group=None, on_frame=None, streams: bool = False,
+                 device=None, depth: int = 2, group=None, on_frame=None, streams=False,
                  gather: bool = None):
         import torch
 
@@ -251,7 +251,13 @@ class FramePipeline:
                                 for g in self.gathered]
                 self.asm_dst = self.frame_padded.view((tpr, world, tile_rows) + tuple(part_shape[1:]))
                 self.asm_done = [torch.cuda.Event() for _ in range(depth)]
-        self.streams = [torch.cuda.Stream(device) for _ in range(depth)] if (self.cuda and streams) else None
+        # streams: True -> `depth` new render streams; a list -> those (a caller that times several
+        # pipelines in one process keeps one set, so every one runs on the same hardware queues)
+        if isinstance(streams, (list, tuple)):
+            assert len(streams) >= depth
+            self.streams = list(streams[:depth]) if self.cuda else None
+        else:
+            self.streams = [torch.cuda.Stream(device) for _ in range(depth)] if (self.cuda and streams) else None
         self.k = 0
 
     @property
