@@ -247,10 +247,12 @@ _RENDER_STREAMS = {}
 
 
 def render_streams(dev, n: int):
-    """The render streams of the frames in flight, made once per process and reused by every line.
-    HIP maps each new stream to the next hardware queue; a line timed on streams made later in the
-    process landed on other queues and ran slower: test3 0.219 ms as the first line, 0.243 ms after
-    test1 on new streams (profiles/r06/s29, s30)."""
+    """--reuse-streams: the render streams of the frames in flight made once per process and reused
+    by every line.  HIP maps each new stream to a hardware queue, and a line's time depends on where
+    its streams land: test3 0.219 ms as the first line, 0.243 ms after test1 on new streams
+    (profiles/r06/s29, s30); reusing the first line's streams gives test3 0.221 ms (s31) but moved
+    the host-visible lines' streams so that two of three test1 instances serialised their split
+    frame's parts (0.80 -> 1.06 ms, s32), so it is not the default."""
     import torch
 
     key = (dev.index or 0, n)
@@ -362,7 +364,8 @@ def measure(workload: str, args, world: int, rank: int, local_rank: int, dev, cp
                 "communicator": "ncclCommInitRank (rg_comm_init_rank; unique id broadcast by torch.distributed)"}
     if not native and use_pipe:
         pipe = rd.FramePipeline((slot, W, 4), H, rank, world, TR, device=dev, depth=F,
-                                streams=render_streams(dev, F) if F > 1 and not args.one_render_stream else False,
+                                streams=(render_streams(dev, F) if args.reuse_streams else True)
+                                if F > 1 and not args.one_render_stream else False,
                                 gather=gather)
 
     def step():
@@ -729,6 +732,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames in flight, each on its own render stream (N>1: their gathers overlap later renders); "
                          "0 = 8")
+    ap.add_argument("--reuse-streams", action="store_true",
+                    help="every line's frames in flight on the same render streams (made once per process)")
     ap.add_argument("--one-render-stream", action="store_true",
                     help="render every frame on one stream (N>1: only the gathers overlap the renders)")
     ap.add_argument("--settle-s", type=float, default=0.3,
