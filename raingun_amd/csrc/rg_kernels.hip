@@ -1573,7 +1573,7 @@ template <int MAXD, bool LSPH, bool LCOLD, int WPS, int LBT, bool F32F, bool BVH
           bool HF = false>
 // LBT: lights per shadow batch on the light path (2, 3; -1: one light), 1: the heavy path.
 // HF: the host-frame features (HOSTF below) with MAXD array frames.  TPW: light path, tiles per wave (0: RG_LIGHT_TILES_PER_WAVE; < 0: persistent waves that take tiles
-// until the queue is empty -- single launches, whose makespan is their slowest wave's tile sum).  Light path (LB > 1): blocks of RG_LIGHT_BLOCK_WAVES waves, at least WPS waves
+// until the queue is empty -- single launches, whose makespan is their slowest wave's tile sum).  Light path (LBT != 1): blocks of RG_LIGHT_BLOCK_WAVES waves, at least WPS waves
 // per SIMD (the second bound is waves per execution unit on AMD); heavy path:
 // one block of 4*WPS waves per CU.  Both cap the VGPRs at 512 / WPS.
 __global__ __launch_bounds__(LBT != 1 ? 64 * RG_LIGHT_BLOCK_WAVES : 256 * WPS, LBT != 1 ? WPS : 1)
