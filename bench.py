@@ -247,12 +247,13 @@ _RENDER_STREAMS = {}
 
 
 def render_streams(dev, n: int):
-    """--reuse-streams: the render streams of the frames in flight made once per process and reused
-    by every line.  HIP maps each new stream to a hardware queue, and a line's time depends on where
-    its streams land: test3 0.219 ms as the first line, 0.243 ms after test1 on new streams
-    (profiles/r06/s29, s30); reusing the first line's streams gives test3 0.221 ms (s31) but moved
-    the host-visible lines' streams so that two of three test1 instances serialised their split
-    frame's parts (0.80 -> 1.06 ms, s32), so it is not the default."""
+    """The render streams of the frames in flight, made once per process and reused by every line
+    (--no-reuse-streams: new ones per line).  HIP maps each new stream to a hardware queue, and a
+    line's time depends on where its streams land: test3 0.219 ms as the first line, 0.243 ms after
+    test1 on new streams (profiles/r06/s29, s30); on the first line's streams 0.218-0.221 ms (s31,
+    s38).  (Reuse first moved the host-visible lines' streams so that their split frames' two
+    parts shared a queue, 0.80 -> 1.06 ms (s32, s36); the library now gives the one-launch part's
+    stream a hardware queue of its own, rg_capi.hip ensure_image_res.)"""
     import torch
 
     key = (dev.index or 0, n)
@@ -732,8 +733,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames in flight, each on its own render stream (N>1: their gathers overlap later renders); "
                          "0 = 8")
-    ap.add_argument("--reuse-streams", action="store_true",
-                    help="every line's frames in flight on the same render streams (made once per process)")
+    ap.add_argument("--reuse-streams", action=argparse.BooleanOptionalAction, default=True,
+                    help="every line's frames in flight on the same render streams, made once per process "
+                         "(--no-reuse-streams: new streams per line)")
     ap.add_argument("--one-render-stream", action="store_true",
                     help="render every frame on one stream (N>1: only the gathers overlap the renders)")
     ap.add_argument("--settle-s", type=float, default=0.3,

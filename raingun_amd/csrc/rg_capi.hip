@@ -1062,7 +1062,26 @@ rg_status ensure_image_res(const rg_scene *s) {
     rg_image_res &r = s->img;
     if (r.cs) return RG_OK;
     bool good = true;
+#if RG_IMAGE_STREAM_CUMASK
+    // The host frame's two render streams run concurrently (split frames: the device part on
+    // rs[0], the one-launch part on rs[1]), so they must not share a hardware queue.  HIP hands a
+    // plain new stream one of the process's shared queues, and where it lands depends on the
+    // streams made before it: two of three test1 instances ran the split frame at 1.06 ms instead
+    // of 0.76-0.80 (the parts serialised) after the bench reused its render streams
+    // (profiles/r06/s32, s36).  A stream with a CU mask (every CU) gets a hardware queue of its
+    // own: rs[1] is made so.  rs[0] stays a plain stream -- the heavy scenes' one-launch frame runs
+    // there, and on a CU-masked queue it measured 2.32 instead of 2.03 ms in two of three runs (s37).
+    {
+        int cus = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+        std::vector<uint32_t> mask((size_t)std::max(1, (cus + 31) / 32), 0xFFFFFFFFu);
+        if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+        good = good && ok(hipStreamCreateWithFlags(&r.rs[0], hipStreamNonBlocking)) &&
+               ok(hipExtStreamCreateWithCUMask(&r.rs[1], (uint32_t)mask.size(), mask.data()));
+    }
+#else
     for (hipStream_t &st : r.rs) good = good && ok(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+#endif
     good = good && ok(hipStreamCreateWithFlags(&r.cs, hipStreamNonBlocking));
     for (hipEvent_t &e : r.ev_done) good = good && ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t &e : r.ev_copy) good = good && ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));

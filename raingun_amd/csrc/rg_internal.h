@@ -56,6 +56,9 @@ struct rg_launch_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
+#ifndef RG_IMAGE_STREAM_CUMASK
+#define RG_IMAGE_STREAM_CUMASK 1  // host-frame render streams with a CU mask: a hardware queue each (rg_capi.hip)
+#endif
 #define RG_IMAGE_STAGE_SLOTS 4  // pinned staging slots of the host-visible image path
 #define RG_IMAGE_MAX_BANDS 16   // events / counter snapshots per host-visible render or stream ring
 #define RG_IMAGE_BAND_PX (2u << 20)    // ~pixels per band of a banded host-visible frame
