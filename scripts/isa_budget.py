@@ -25,7 +25,7 @@ Dynamic side (--visits region_stats.json from scripts/region_stats.py): each reg
 times its static instructions = the dynamic count; the sum is reconciled with the PMC counters
 (SQ_INSTS_VALU, the FP64 counters) of the same frame.
 
-    python scripts/isa_budget.py [--kernel MANGLED] [--visits stats.json] [--json out.json] [hipcc flags...]
+    python scripts/isa_budget.py [--kernel MANGLED] [--heavy] [--visits stats.json] [--json out.json] [hipcc flags...]
 """
 import collections
 import json
@@ -180,13 +180,17 @@ def main():
             del args[k:k + 2]
             kernel, out_json, visits_path = ((v, out_json, visits_path) if flag == "--kernel" else
                                              (kernel, v, visits_path) if flag == "--json" else (kernel, out_json, v))
+    dev_only = "-DRG_DEV_LIGHT_ONLY"
+    if "--heavy" in args:  # the heavy-path instantiations (give their --kernel)
+        args.remove("--heavy")
+        dev_only = "-DRG_DEV_HEAVY_ONLY"
     build = "stats"
     if "--build" in args:
         k = args.index("--build"); build = args[k + 1]; del args[k:k + 2]
     tmp = Path("/tmp/rg_isa_budget")
     tmp.mkdir(exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
-           "-fPIC", "-gline-tables-only", "-DRG_DEV_LIGHT_ONLY", "-DRG_DEV_ONE_DEPTH", "-c", "rg_kernels.hip",
+           "-fPIC", "-gline-tables-only", dev_only, "-DRG_DEV_ONE_DEPTH", "-c", "rg_kernels.hip",
            "-o", str(tmp / "k.o"), "--save-temps=obj", *(["-DRG_REGION_STATS"] if build == "stats" else []), *args]
     r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)
     if r.returncode != 0:
