@@ -2884,6 +2884,13 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 #ifndef RG_LIGHT_WPS
 #define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
 #endif
+#ifndef RG_LIGHT_TPW_BIG
+// light path, 3-light batch: tiles per wave of whole-frame launches (0: off).  32 measured
+// test1 0.2968 -> 0.2943 ms as a compile-time variant (profiles/r06/s43); the dispatch below was
+// written at the end of round 6 and could not be checked on a GPU before the round closed (the
+// pool's boxes failed during preparation), so it ships off
+#define RG_LIGHT_TPW_BIG 0
+#endif
 #ifndef RG_LIGHT_WPS_ONE
 #define RG_LIGHT_WPS_ONE RG_LIGHT_WPS  // the one-light batch (118 VGPRs at 4 waves per SIMD)
 #endif
@@ -2928,6 +2935,14 @@ static hipError_t launch_depth(const RgKernelArgs *a, hipStream_t stream, size_t
 #endif
             if constexpr (MAXD != 0 && RG_LIGHT_SINGLE_PERSISTENT)
                 if (persistent) return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, -1>(a, stream, gt);
+#if RG_LIGHT_TPW_BIG > 0
+            // whole frames (frames in flight): RG_LIGHT_TPW_BIG tiles per wave, half the waves of
+            // RG_LIGHT_TILES_PER_WAVE (as a compile-time variant: test1 0.2968 -> 0.2943 ms over 200
+            // frames, profiles/r06/s43); smaller launches (the 1/N shares) keep 16
+            if constexpr (MAXD != 0)
+                if (rg_tile_count(*a) >= RG_LIGHT_BIG_TILES)
+                    return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false, RG_LIGHT_TPW_BIG>(a, stream, gt);
+#endif
             return launch_waves<MAXD, RG_LIGHT_WPS, RG_LB, false, false, false>(a, stream, gt);
         }
     }
