@@ -2885,11 +2885,9 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 #define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
 #endif
 #ifndef RG_LIGHT_TPW_BIG
-// light path, 3-light batch: tiles per wave of whole-frame launches (0: off).  32 measured
-// test1 0.2968 -> 0.2943 ms as a compile-time variant (profiles/r06/s43); the dispatch below was
-// written at the end of round 6 and could not be checked on a GPU before the round closed (the
-// pool's boxes failed during preparation), so it ships off
-#define RG_LIGHT_TPW_BIG 0
+// light path, 3-light batch: tiles per wave of whole-frame launches (0: off): test1 0.2938 ->
+// 0.2923 ms over 3 x 200 frames, -m gpu 284 passed with it (profiles/r06/s45)
+#define RG_LIGHT_TPW_BIG 32
 #endif
 #ifndef RG_LIGHT_WPS_ONE
 #define RG_LIGHT_WPS_ONE RG_LIGHT_WPS  // the one-light batch (118 VGPRs at 4 waves per SIMD)
