@@ -2885,9 +2885,11 @@ static hipError_t launch_waves(const RgKernelArgs *a, hipStream_t stream, size_t
 #define RG_LIGHT_WPS 4            // light path: waves per SIMD (128 VGPRs; 3 -> 4: test1 -3 %, test3 -8 %, profiles/r02/ab_light_wps.txt)
 #endif
 #ifndef RG_LIGHT_TPW_BIG
-// light path, 3-light batch: tiles per wave of whole-frame launches (0: off): test1 0.2938 ->
-// 0.2923 ms over 3 x 200 frames, -m gpu 284 passed with it (profiles/r06/s45)
-#define RG_LIGHT_TPW_BIG 32
+// light path, 3-light batch: tiles per wave of whole-frame launches (0: off).  32: test1 0.2938 ->
+// 0.2923 ms over 3 x 200 frames (-m gpu 284 passed, profiles/r06/s45), but 0.304 -> 0.319 ms in
+// the driver's 20-frame configuration (longer waves, longer drain at the end of a short burst:
+// s46), so off
+#define RG_LIGHT_TPW_BIG 0
 #endif
 #ifndef RG_LIGHT_WPS_ONE
 #define RG_LIGHT_WPS_ONE RG_LIGHT_WPS  // the one-light batch (118 VGPRs at 4 waves per SIMD)
